@@ -1,0 +1,174 @@
+"""ORACLE (test infrastructure only) -- CPU restatement of bellman 0.1.0 ``groth16``.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as a checker; the product path never does.
+
+Restates (bellman is not vendored; pinned ``crypto/Cargo.toml:7``, ``Cargo.lock:79-91``):
+  * ``Proof::<Bls12>::read``       -- called at verification/src/sapling.rs:158,203 and
+                                      crypto/src/groth16.rs:54
+  * ``prepare_verifying_key``      -- crypto/src/json/groth16.rs:14,21,27
+  * ``verify_proof``               -- verification/src/sapling.rs:162,207, sprout.rs:73-77
+  * the VK JSON loader             -- crypto/src/json/groth16.rs:11-102 (serde + Point<EP>)
+plus the batch semantics of this build: with batch scalars r_i the
+accumulated GT of a batch equals prod_i LHS_i^{r_i}, LHS_i being bellman's per-proof
+final-exponentiated left-hand side.
+"""
+import hashlib
+import json
+
+from . import bls12_381 as B
+
+SPEND, OUTPUT, SPROUT = 0, 1, 2
+KIND_NAMES = {SPEND: "spend", OUTPUT: "output", SPROUT: "sprout"}
+KIND_NINPUTS = {SPEND: 7, OUTPUT: 5, SPROUT: 9}
+
+# per-proof status codes of the C ABI (include/zg.h)
+OK, DECODE_INVALID, MALFORMED_VK, VERIFY_FAILED, INPUT_NONCANONICAL = 0, 1, 2, 3, 4
+
+
+class SynthesisError(Exception):
+    """bellman SynthesisError::MalformedVerifyingKey."""
+
+
+class VerifyingKey:
+    def __init__(self, alpha_g1, beta_g1, beta_g2, gamma_g2, delta_g1, delta_g2, ic):
+        self.alpha_g1, self.beta_g1, self.beta_g2 = alpha_g1, beta_g1, beta_g2
+        self.gamma_g2, self.delta_g1, self.delta_g2 = gamma_g2, delta_g1, delta_g2
+        self.ic = list(ic)
+
+
+class PreparedVerifyingKey:
+    def __init__(self, vk):
+        self.vk = vk
+        self.alpha_g1_beta_g2 = B.pairing(vk.alpha_g1, vk.beta_g2)
+        self.neg_gamma_g2 = B.g2_prepare(B.ec_neg(B.FQ2, vk.gamma_g2))
+        self.neg_delta_g2 = B.g2_prepare(B.ec_neg(B.FQ2, vk.delta_g2))
+        self.ic = list(vk.ic)
+
+
+def prepare_verifying_key(vk):
+    return PreparedVerifyingKey(vk)
+
+
+def _clean_0x(s):
+    return s[2:] if s.startswith("0x") else s
+
+
+def load_vk_json(text):
+    """crypto/src/json/groth16.rs:33-102 -- hex strings decoded as *uncompressed* points
+    with on-curve and subgroup checks (any failure is an error)."""
+    d = json.loads(text)
+
+    def g1(h):
+        raw = bytes.fromhex(_clean_0x(h))
+        if len(raw) != 96:
+            raise B.DecodeError("Expected hex string of length 96")
+        return B.g1_decode_uncompressed(raw)
+
+    def g2(h):
+        raw = bytes.fromhex(_clean_0x(h))
+        if len(raw) != 192:
+            raise B.DecodeError("Expected hex string of length 192")
+        return B.g2_decode_uncompressed(raw)
+
+    return VerifyingKey(g1(d["alphaG1"]), g1(d["betaG1"]), g2(d["betaG2"]), g2(d["gammaG2"]),
+                        g1(d["deltaG1"]), g2(d["deltaG2"]), [g1(x) for x in d["ic"]])
+
+
+def bad_verifying_key():
+    """verification/src/sapling.rs:345-358: all-zero points, empty ic."""
+    return VerifyingKey(None, None, None, None, None, None, [])
+
+
+def proof_read(data):
+    """bellman Proof::read: A (G1 48 B) || B (G2 96 B) || C (G1 48 B), compressed,
+    each into_affine (subgroup-checked), infinity rejected."""
+    assert len(data) == 192
+    a = B.g1_decompress(data[0:48])
+    if a is None:
+        raise B.DecodeError("point at infinity")
+    b = B.g2_decompress(data[48:144])
+    if b is None:
+        raise B.DecodeError("point at infinity")
+    c = B.g1_decompress(data[144:192])
+    if c is None:
+        raise B.DecodeError("point at infinity")
+    return (a, b, c)
+
+
+def compute_acc(pvk, inputs):
+    acc = pvk.ic[0]
+    for x, base in zip(inputs, pvk.ic[1:]):
+        acc = B.ec_add(B.FQ, acc, B.ec_mul(B.FQ, base, x))
+    return acc
+
+
+def lhs_gt(pvk, proof, inputs):
+    """final_exponentiation(miller_loop([(A, B), (acc, -gamma), (C, -delta)]))."""
+    if len(inputs) + 1 != len(pvk.ic):
+        raise SynthesisError("MalformedVerifyingKey")
+    a, b, c = proof
+    acc = compute_acc(pvk, inputs)
+    f = B.miller_loop([(a, B.g2_prepare(b)), (acc, pvk.neg_gamma_g2), (c, pvk.neg_delta_g2)])
+    return B.final_exponentiation(f)
+
+
+def verify_proof(pvk, proof, inputs):
+    return lhs_gt(pvk, proof, inputs) == pvk.alpha_g1_beta_g2
+
+
+def verify_status(pvk, proof_bytes, inputs, n_inputs=None):
+    """Per-proof status as the C ABI reports it, with the reference's precedence
+    (sapling.rs:157-167: Proof::read before verify_proof's input-count check)."""
+    if any(x >= B.R for x in inputs):
+        return INPUT_NONCANONICAL, None
+    try:
+        proof = proof_read(proof_bytes)
+    except B.DecodeError:
+        return DECODE_INVALID, None
+    k = len(inputs) if n_inputs is None else n_inputs
+    if k + 1 != len(pvk.ic):
+        return MALFORMED_VK, None
+    gt = lhs_gt(pvk, proof, inputs[:k])
+    return (OK if gt == pvk.alpha_g1_beta_g2 else VERIFY_FAILED), gt
+
+
+# ----------------------------------------------------------------------------- synthetic data
+def rerandomize_scalars(seed, i):
+    """t, s in Fr\\{0} from BLAKE2b-512("zg-rerand" || seed_le64 || i_le64)."""
+    h = hashlib.blake2b(b"zg-rerand" + seed.to_bytes(8, "little") + i.to_bytes(8, "little"),
+                        digest_size=64).digest()
+    t = int.from_bytes(h[:32], "little") % B.R or 1
+    s = int.from_bytes(h[32:], "little") % B.R or 1
+    return t, s
+
+
+def batch_scalar(seed, i):
+    """128-bit non-zero r_i from BLAKE2b-128("zg-batch-r" || seed_le64 || i_le64)."""
+    h = hashlib.blake2b(b"zg-batch-r" + seed.to_bytes(8, "little") + i.to_bytes(8, "little"),
+                        digest_size=16).digest()
+    return int.from_bytes(h, "little") or 1
+
+
+def rerandomize(proof, delta_g2, t, s):
+    """(A, B, C) -> (t^-1 A, t B + t s delta, C + s A): valid iff the source is
+    (e(A',B') = e(A,B) e(sA, delta), C' = C + sA)."""
+    a, b, c = proof
+    ti = pow(t, B.R - 2, B.R)
+    a2 = B.ec_mul(B.FQ, a, ti)
+    b2 = B.ec_add(B.FQ2, B.ec_mul(B.FQ2, b, t), B.ec_mul(B.FQ2, delta_g2, t * s % B.R))
+    c2 = B.ec_add(B.FQ, c, B.ec_mul(B.FQ, a, s))
+    return (a2, b2, c2)
+
+
+def proof_bytes(proof):
+    a, b, c = proof
+    return B.g1_compress(a) + B.g2_compress(b) + B.g1_compress(c)
+
+
+def batch_gt(lhs_list, r_list):
+    """accumulated GT of a batch: prod LHS_i^{r_i}."""
+    acc = B.F12_ONE
+    for gt, r in zip(lhs_list, r_list):
+        acc = B.f12_mul(acc, B.f12_pow(gt, r))
+    return acc

@@ -1,0 +1,351 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ from the oracle.
+
+Run in the survey container (needs /root/reference, read as TEXT only: the real mainnet
+transactions/blocks and test fields are extracted from the reference's test sources and
+stored here as data -- proof bytes, description fields, expected statuses/GT).
+
+    python tests/golden/gen_golden.py
+
+Sources (reference file:line):
+  * tx bd4fe81c... (1 spend + 1 output)      verification/src/sapling.rs:303-305, test at :360-363
+  * smoky_groth Sprout-Groth16 JoinSplit     verification/src/sprout.rs:356-396
+  * block 419221 (+ donors)                  test-data/src/lib.rs:117-131
+  * hSig vectors / bit order                 verification/src/sprout.rs:198-289
+  * reference mutants                        verification/src/sapling.rs:365-510
+"""
+import json
+import os
+import re
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import bls12_381 as B, groth16 as G, zcash as Z  # noqa: E402
+
+REF = "/root/reference"
+VK_FILES = {G.SPEND: "sapling-spend-verifying-key.json", G.OUTPUT: "sapling-output-verifying-key.json",
+            G.SPROUT: "sprout-groth16-key.json"}
+
+
+def hx(b):
+    return b.hex()
+
+
+def fr_hex(v):
+    return v.to_bytes(32, "little").hex()
+
+
+def load_pvks():
+    return {k: G.prepare_verifying_key(G.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", f)).read()))
+            for k, f in VK_FILES.items()}
+
+
+def extract_sources():
+    sap = open(os.path.join(REF, "verification/src/sapling.rs")).read()
+    tx_hex = re.search(r'"(0400008085202f89[0-9a-f]+)"\.into\(\)', sap).group(1)
+    spr = open(os.path.join(REF, "verification/src/sprout.rs")).read()
+    body = spr[spr.index("fn smoky_groth()"):]
+    groth_hex = re.search(r'groth16_proof\("([0-9a-f]{384})"\)', spr).group(1)
+
+    def field(name):
+        return bytes.fromhex(re.search(name + r': hash2\("([0-9a-f]{64})"\)', body).group(1))
+
+    h2 = re.findall(r'hash2\("([0-9a-f]{64})"\)', body)
+    smoky = {
+        "vpub_new": int(re.search(r"value_pub_new: (\d+)", body).group(1)),
+        "vpub_old": int(re.search(r"value_pub_old: (\d+)", body).group(1)),
+        "anchor": field("anchor"),
+        "nullifiers": [bytes.fromhex(h2[1]), bytes.fromhex(h2[2])],
+        "commitments": [bytes.fromhex(h2[3]), bytes.fromhex(h2[4])],
+        "random_seed": field("random_seed"),
+        "macs": [bytes.fromhex(h2[6]), bytes.fromhex(h2[7])],
+        "zkproof": bytes.fromhex(groth_hex),
+        "groth": True,
+    }
+    smoky_pubkey = bytes.fromhex(re.search(r'pubkey: hash2\("([0-9a-f]{64})"\)', body).group(1))
+    lib = open(os.path.join(REF, "test-data/src/lib.rs")).read()
+    fn = lib[lib.index("pub fn block_h419221_with_donors"):]
+    hexes = re.findall(r'"([0-9a-f]{200,})"', fn[:fn.index("\n}\n")])
+    return tx_hex, smoky, smoky_pubkey, hexes[0], hexes[1:]
+
+
+def g1_nonsubgroup(start):
+    x = start
+    while True:
+        y = B.fq_sqrt((x ** 3 + 4) % B.P)
+        if y is not None and not B.g1_in_subgroup((x, y)):
+            return (x, y)
+        x += 1
+
+
+def g2_nonsubgroup(start):
+    x0 = start
+    while True:
+        x = (x0, 1)
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B2))
+        if y is not None and not B.g2_in_subgroup((x, y)):
+            return (x, y)
+        x0 += 1
+
+
+def g1_not_on_curve_x(start):
+    x = start
+    while B.fq_sqrt((x ** 3 + 4) % B.P) is not None:
+        x += 1
+    return x
+
+
+def raw_g1_nocheck(pt, greatest=None):
+    """compressed encoding of an on-curve point without any subgroup assumption."""
+    return B.g1_compress(pt)
+
+
+def main():
+    pvks = load_pvks()
+    tx_hex, smoky, smoky_pubkey, block_hex, donors = extract_sources()
+
+    # ---------------------------------------------------------------- real proofs
+    real = []
+    tx = Z.parse_tx_hex(tx_hex)
+    assert tx["txid"].startswith("bd4fe81c")
+    s = tx["spends"][0]
+    o = tx["outputs"][0]
+    tx_fields = {"spends": [], "outputs": [], "joinsplits": []}
+
+    def add_spend(name, txid, s):
+        inp = Z.spend_inputs(s["cv"], s["anchor"], s["nullifier"], s["rk"])
+        real.append({"name": name, "txid": txid, "kind": G.SPEND, "proof": hx(s["zkproof"]),
+                     "inputs": [fr_hex(v) for v in inp]})
+        tx_fields["spends"].append({"name": name, "cv": hx(s["cv"]), "anchor": hx(s["anchor"]),
+                                    "nullifier": hx(s["nullifier"]), "rk": hx(s["rk"]),
+                                    "zkproof": hx(s["zkproof"]), "inputs": [fr_hex(v) for v in inp]})
+
+    def add_output(name, txid, o):
+        inp = Z.output_inputs(o["cv"], o["cmu"], o["epk"])
+        real.append({"name": name, "txid": txid, "kind": G.OUTPUT, "proof": hx(o["zkproof"]),
+                     "inputs": [fr_hex(v) for v in inp]})
+        tx_fields["outputs"].append({"name": name, "cv": hx(o["cv"]), "cmu": hx(o["cmu"]),
+                                     "epk": hx(o["epk"]), "zkproof": hx(o["zkproof"]),
+                                     "inputs": [fr_hex(v) for v in inp]})
+
+    def add_js(name, txid, d, pubkey):
+        inp = Z.sprout_inputs(d, pubkey)
+        real.append({"name": name, "txid": txid, "kind": G.SPROUT, "proof": hx(d["zkproof"]),
+                     "inputs": [fr_hex(v) for v in inp]})
+        tx_fields["joinsplits"].append({
+            "name": name, "vpub_old": d["vpub_old"], "vpub_new": d["vpub_new"], "anchor": hx(d["anchor"]),
+            "nullifiers": [hx(x) for x in d["nullifiers"]], "commitments": [hx(x) for x in d["commitments"]],
+            "random_seed": hx(d["random_seed"]), "macs": [hx(x) for x in d["macs"]], "pubkey": hx(pubkey),
+            "zkproof": hx(d["zkproof"]), "inputs": [fr_hex(v) for v in inp]})
+
+    add_spend("S1", tx["txid"], s)
+    add_output("O1", tx["txid"], o)
+    add_js("J1", "smoky_groth", smoky, smoky_pubkey)
+
+    bhash, btxs = Z.parse_block_hex(block_hex)
+    blk_items = {"S": [], "O": [], "J": []}
+    for t in btxs:
+        for d in t["joinsplits"]:
+            if d["groth"]:
+                blk_items["J"].append((t["txid"], d, t["js_pubkey"]))
+        for sp in t["spends"]:
+            blk_items["S"].append((t["txid"], sp))
+        for op in t["outputs"]:
+            blk_items["O"].append((t["txid"], op))
+    for i, (txid, sp) in enumerate(blk_items["S"]):
+        add_spend("S%d" % (2 + i), txid, sp)
+    for i, (txid, op) in enumerate(blk_items["O"]):
+        add_output("O%d" % (2 + i), txid, op)
+    for i, (txid, d, pk) in enumerate(blk_items["J"]):
+        add_js("J%d" % (2 + i), txid, d, pk)
+
+    for e in real:
+        inp = [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]]
+        st, gt = G.verify_status(pvks[e["kind"]], bytes.fromhex(e["proof"]), inp)
+        e["status"] = st
+        e["lhs_gt"] = hx(B.f12_to_bytes(gt))
+        print(e["name"], e["txid"][:8], G.KIND_NAMES[e["kind"]], "status", st, flush=True)
+        assert st == G.OK, e["name"]
+
+    # ---------------------------------------------------------------- VK facts
+    vkinfo = {}
+    for k, pvk in pvks.items():
+        vkinfo[G.KIND_NAMES[k]] = {"file": VK_FILES[k], "ic_len": len(pvk.ic),
+                                   "alpha_g1_beta_g2": hx(B.f12_to_bytes(pvk.alpha_g1_beta_g2))}
+    vkinfo["shared_alpha_beta_gamma"] = all(
+        pvks[0].vk.alpha_g1 == v.vk.alpha_g1 and pvks[0].vk.beta_g2 == v.vk.beta_g2
+        and pvks[0].vk.gamma_g2 == v.vk.gamma_g2 for v in pvks.values())
+    vkinfo["block_419221_hash"] = bhash
+
+    # ---------------------------------------------------------------- proof mutants
+    mutants = []
+
+    def mut(name, kind, proof, inputs, vk="builtin", n_inputs=None, pinned=None):
+        pvk = pvks[kind] if vk == "builtin" else G.prepare_verifying_key(G.bad_verifying_key())
+        st, gt = G.verify_status(pvk, proof, inputs, n_inputs)
+        mutants.append({"name": name, "kind": kind, "proof": hx(proof), "inputs": [fr_hex(v) for v in inputs],
+                        "vk": vk, "status": st, "lhs_gt": hx(B.f12_to_bytes(gt)) if gt is not None else None,
+                        "pinned_by": pinned})
+        print("mutant", name, "->", st, flush=True)
+
+    by_name = {e["name"]: e for e in real}
+    ng1 = g1_nonsubgroup(1)
+    ng2 = g2_nonsubgroup(1)
+    bad_x = g1_not_on_curve_x(2)
+    for src in ("S1", "O1", "J1"):
+        e = by_name[src]
+        kind = e["kind"]
+        pf = bytes.fromhex(e["proof"])
+        inp = [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]]
+        A, Bp, C = pf[:48], pf[48:144], pf[144:]
+        mut(src + ":zero_proof", kind, bytes(192), inp, pinned="verification/src/sapling.rs:420-426,486-492")
+        mut(src + ":bad_vk_empty_ic", kind, pf, inp, vk="bad", pinned="verification/src/sapling.rs:428-432,494-501")
+        mut(src + ":input0_plus1", kind, pf, [(inp[0] + 1) % B.R] + inp[1:])
+        mut(src + ":input_last_noncanonical", kind, pf, inp[:-1] + [B.R])
+        mut(src + ":A_flag_cleared", kind, bytes([A[0] & 0x7F]) + A[1:] + Bp + C, inp)
+        mut(src + ":B_flag_cleared", kind, A + bytes([Bp[0] & 0x7F]) + Bp[1:] + C, inp)
+        mut(src + ":A_infinity", kind, bytes([0xC0]) + bytes(47) + Bp + C, inp)
+        mut(src + ":B_infinity", kind, A + bytes([0xC0]) + bytes(95) + C, inp)
+        mut(src + ":C_infinity", kind, A + Bp + bytes([0xC0]) + bytes(47), inp)
+        mut(src + ":A_infinity_garbage", kind, bytes([0xC0]) + bytes(46) + b"\x01" + Bp + C, inp)
+        mut(src + ":A_infinity_flag_on_valid", kind, bytes([A[0] | 0x40]) + A[1:] + Bp + C, inp)
+        mut(src + ":A_x_ge_p", kind, bytes([0x80 | 0x1A]) + (B.P + 5).to_bytes(48, "big")[1:] + Bp + C, inp)
+        xp = bytearray((B.P + 3).to_bytes(48, "big"))
+        xp[0] |= 0x80
+        mut(src + ":B_x_c1_ge_p", kind, A + bytes(xp) + Bp[48:] + C, inp)
+        mut(src + ":B_x_c0_ge_p", kind, A + Bp[:48] + (B.P + 3).to_bytes(48, "big") + C, inp)
+        ax = bytearray(bad_x.to_bytes(48, "big"))
+        ax[0] |= 0x80
+        mut(src + ":A_not_on_curve", kind, bytes(ax) + Bp + C, inp)
+        mut(src + ":A_not_in_subgroup", kind, B.g1_compress(ng1) + Bp + C, inp)
+        mut(src + ":C_not_in_subgroup", kind, A + Bp + B.g1_compress(ng1), inp)
+        mut(src + ":B_not_in_subgroup", kind, A + B.g2_compress(ng2) + C, inp)
+        mut(src + ":A_sign_flipped", kind, bytes([A[0] ^ 0x20]) + A[1:] + Bp + C, inp)
+        mut(src + ":B_sign_flipped", kind, A + bytes([Bp[0] ^ 0x20]) + Bp[1:] + C, inp)
+        mut(src + ":C_sign_flipped", kind, A + Bp + bytes([C[0] ^ 0x20]) + C[1:], inp)
+        mut(src + ":A_C_swapped", kind, C + Bp + A, inp)
+        cx = bytearray(C)
+        cx[47] ^= 0x01
+        mut(src + ":C_x_bitflip", kind, A + Bp + bytes(cx), inp)
+        other = G.OUTPUT if kind != G.OUTPUT else G.SPEND
+        mut(src + ":wrong_kind_vk", other, pf, inp)
+    # reference-pinned description-level Groth16 failures (sapling.rs:434-440, 504-509)
+    s1 = tx_fields["spends"][0]
+    nf0 = Z.spend_inputs(bytes.fromhex(s1["cv"]), bytes.fromhex(s1["anchor"]), bytes(32), bytes.fromhex(s1["rk"]))
+    mut("S1:nullifier_zeroed", G.SPEND, bytes.fromhex(s1["zkproof"]), nf0,
+        pinned="verification/src/sapling.rs:434-440")
+    o1 = tx_fields["outputs"][0]
+    cm = Z.output_inputs(bytes.fromhex(o1["cv"]), bytes.fromhex(o1["cv"]), bytes.fromhex(o1["epk"]))
+    mut("O1:cmu_is_cv", G.OUTPUT, bytes.fromhex(o1["zkproof"]), cm, pinned="verification/src/sapling.rs:504-509")
+
+    # ---------------------------------------------------------------- host input-prep vectors
+    def prep_err(fn, *a):
+        try:
+            fn(*a)
+            return None
+        except Z.InputError as e:
+            return e.where
+
+    def swap_xy(b):
+        return b[16:] + b[:16]
+    prep = []
+    sb = {k: bytes.fromhex(v) for k, v in s1.items() if k in ("cv", "anchor", "nullifier", "rk")}
+    for name, ch, want, where in [
+            ("cv_swap_xy", {"cv": swap_xy(sb["cv"])}, "ValueCommitment(Invalid)", "sapling.rs:371-377"),
+            ("cv_small_order", {"cv": bytes(32)}, "ValueCommitment(SmallOrder)", "sapling.rs:379-385"),
+            ("anchor_not_in_field", {"anchor": b"\xff" * 32}, "Anchor", "sapling.rs:387-393"),
+            ("rk_swap_xy", {"rk": swap_xy(sb["rk"])}, "RandomizedKey(Invalid)", "sapling.rs:395-401"),
+            ("rk_small_order", {"rk": bytes(32)}, "RandomizedKey(SmallOrder)", "sapling.rs:403-409")]:
+        d = dict(sb)
+        d.update(ch)
+        got = prep_err(Z.spend_inputs, d["cv"], d["anchor"], d["nullifier"], d["rk"])
+        assert got == want, (name, got)
+        prep.append({"kind": "spend", "name": name, "fields": {k: hx(v) for k, v in d.items()}, "error": want,
+                     "pinned_by": "verification/src/" + where})
+    ob = {k: bytes.fromhex(v) for k, v in o1.items() if k in ("cv", "cmu", "epk")}
+    for name, ch, want, where in [
+            ("cv_swap_xy", {"cv": swap_xy(sb["cv"])}, "ValueCommitment(Invalid)", "sapling.rs:449-455"),
+            ("cv_small_order", {"cv": bytes(32)}, "ValueCommitment(SmallOrder)", "sapling.rs:457-463"),
+            ("cmu_not_in_field", {"cmu": b"\xff" * 32}, "NoteCommitment", "sapling.rs:465-471"),
+            ("epk_swap_xy", {"epk": swap_xy(ob["epk"])}, "EphemeralKey(Invalid)", "sapling.rs:473-479"),
+            ("epk_small_order", {"epk": bytes(32)}, "EphemeralKey(SmallOrder)", "sapling.rs:481-487")]:
+        d = dict(ob)
+        d.update(ch)
+        got = prep_err(Z.output_inputs, d["cv"], d["cmu"], d["epk"])
+        assert got == want, (name, got)
+        prep.append({"kind": "output", "name": name, "fields": {k: hx(v) for k, v in d.items()}, "error": want,
+                     "pinned_by": "verification/src/" + where})
+
+    # hSig known answers (sprout.rs:198-260; `hash()` reverses the hex bytes)
+    def rev(h):
+        return bytes.fromhex(h)[::-1]
+    spr = open(os.path.join(REF, "verification/src/sprout.rs")).read()
+    tv = spr[spr.index("fn test_vectors()"):spr.index("fn input_to_str")]
+    hs = []
+    for blk in tv.split("compute_hsig(")[1:]:
+        h = re.findall(r'hash\("([0-9a-f]{64})"\)', blk)
+        seed, n0, n1, pk, want = (rev(x) for x in h[:5])
+        got = Z.compute_hsig(seed, n0, n1, pk)
+        assert got == want
+        hs.append({"random_seed": hx(seed), "nullifiers": [hx(n0), hx(n1)], "pubkey": hx(pk), "hsig": hx(want)})
+    bit1 = [b for byte in bytes([0x00, 0x01, 0x03, 0x12, 0xFF]) for b in ((byte >> i) & 1 for i in range(7, -1, -1))]
+    assert "".join(map(str, bit1)) == "0000000000000001000000110001001011111111"   # sprout.rs:269-278
+
+    # ---------------------------------------------------------------- seeded batch (with corruptions)
+    seed = 7
+    srcs = ["S1", "S2", "O1", "O2", "O3", "J1", "J2", "J3", "J4"]
+    batch = {"seed": seed, "r_seed": seed, "items": []}
+    lhs, rs = [], []
+    corrupt = {5: "A_sign_flipped", 17: "input0_plus1", 30: "B_not_in_subgroup", 41: "A_C_swapped",
+               58: "zero_proof"}
+    for i in range(64):
+        e = by_name[srcs[i % len(srcs)]]
+        kind = e["kind"]
+        inp = [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]]
+        t, s_ = G.rerandomize_scalars(seed, i)
+        pr = G.rerandomize(G.proof_read(bytes.fromhex(e["proof"])), pvks[kind].vk.delta_g2, t, s_)
+        pb = G.proof_bytes(pr)
+        c = corrupt.get(i)
+        if c == "A_sign_flipped":
+            pb = bytes([pb[0] ^ 0x20]) + pb[1:]
+        elif c == "input0_plus1":
+            inp = [(inp[0] + 1) % B.R] + inp[1:]
+        elif c == "B_not_in_subgroup":
+            pb = pb[:48] + B.g2_compress(ng2) + pb[144:]
+        elif c == "A_C_swapped":
+            pb = pb[144:] + pb[48:144] + pb[:48]
+        elif c == "zero_proof":
+            pb = bytes(192)
+        r = G.batch_scalar(seed, i)
+        st, gt = G.verify_status(pvks[kind], pb, inp)
+        batch["items"].append({"src": e["name"], "kind": kind, "proof": hx(pb), "inputs": [fr_hex(v) for v in inp],
+                               "r": r.to_bytes(16, "little").hex(), "status": st, "corruption": c,
+                               "lhs_gt": hx(B.f12_to_bytes(gt)) if gt is not None else None})
+        if st in (G.OK, G.VERIFY_FAILED):
+            lhs.append(gt)
+            rs.append(r)
+        print("batch", i, st, flush=True)
+    batch["gt_out"] = hx(B.f12_to_bytes(G.batch_gt(lhs, rs)))
+    batch["gt_out_def"] = "prod over proofs with status OK or VERIFY_FAILED of lhs_gt^r"
+
+    # all-valid sub-batch (first 64 without corruptions) accumulated GT
+    out = {
+        "real_proofs.json": {"source": "oracle/groth16.py on reference fixtures", "proofs": real},
+        "mutants.json": {"mutants": mutants},
+        "vk.json": vkinfo,
+        "input_prep.json": {"tx_fields": tx_fields, "prep_errors": prep, "hsig": hs},
+        "batch64.json": batch,
+        "points.json": {"g1_not_in_subgroup": hx(B.g1_compress(ng1)), "g2_not_in_subgroup": hx(B.g2_compress(ng2)),
+                        "g1_not_on_curve_x": hex(bad_x)},
+    }
+    for fn, obj in out.items():
+        with open(os.path.join(HERE, fn), "w") as f:
+            json.dump(obj, f, indent=1, sort_keys=True)
+        print("wrote", fn)
+
+
+if __name__ == "__main__":
+    main()
