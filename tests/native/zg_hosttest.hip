@@ -1,0 +1,101 @@
+// TEST HARNESS ONLY -- runs the product's __host__ __device__ arithmetic (zebra_amd/csrc)
+// on the CPU so the CPU-only test tier can check it against the oracle without a GPU.
+// Never linked into, or loaded by, the product library.
+#include <string.h>
+#include "../../zebra_amd/csrc/zg_groth16.h"
+
+using namespace zg;
+
+static Fq ld_fq(const uint8_t* b) { return fq_to_mont(fq_limbs_from_be(b)); }
+static void st_fq(const Fq& a, uint8_t* b) { fq_limbs_to_be(fq_from_mont(a), b); }
+
+extern "C" {
+
+void zgt_fq_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_mul(ld_fq(a), ld_fq(b)), out); }
+void zgt_fq_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_add(ld_fq(a), ld_fq(b)), out); }
+void zgt_fq_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_sub(ld_fq(a), ld_fq(b)), out); }
+void zgt_fq_inv(const uint8_t* a, uint8_t* out) { st_fq(fq_inv(ld_fq(a)), out); }
+int zgt_fq_sqrt(const uint8_t* a, uint8_t* out) {
+  Fq s;
+  bool ok = fq_sqrt(ld_fq(a), &s);
+  st_fq(s, out);
+  return ok;
+}
+void zgt_fr_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  Fr x = fr_to_mont(fr_limbs_from_le(a)), y = fr_to_mont(fr_limbs_from_le(b));
+  Fr r = fr_from_mont(fr_mul(x, y));
+  memcpy(out, r.l, 32);
+}
+void zgt_f12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  f12_to_bytes(f12_mul(f12_from_bytes(a), f12_from_bytes(b)), out);
+}
+void zgt_f12_sqr(const uint8_t* a, uint8_t* out) { f12_to_bytes(f12_sqr(f12_from_bytes(a)), out); }
+void zgt_f12_inv(const uint8_t* a, uint8_t* out) { f12_to_bytes(f12_inv(f12_from_bytes(a)), out); }
+void zgt_f12_frob(const uint8_t* a, int k, uint8_t* out) { f12_to_bytes(f12_frob(f12_from_bytes(a), k), out); }
+void zgt_final_exp(const uint8_t* a, uint8_t* out) { f12_to_bytes(final_exponentiation(f12_from_bytes(a)), out); }
+int zgt_f2_sqrt(const uint8_t* a, uint8_t* out) {
+  Fq2 x = {ld_fq(a), ld_fq(a + 48)}, s;
+  bool ok = f2_sqrt(x, &s);
+  st_fq(s.c0, out);
+  st_fq(s.c1, out + 48);
+  return ok;
+}
+
+// decode: returns DEC_* ; writes affine x||y (canonical BE)
+int zgt_g1_decompress(const uint8_t* b, uint8_t* out) {
+  G1A p;
+  int r = g1_decompress(b, &p);
+  if (r == DEC_OK) {
+    st_fq(p.x, out);
+    st_fq(p.y, out + 48);
+  }
+  return r;
+}
+int zgt_g2_decompress(const uint8_t* b, uint8_t* out) {
+  G2A p;
+  int r = g2_decompress(b, &p);
+  if (r == DEC_OK) {
+    st_fq(p.x.c0, out);
+    st_fq(p.x.c1, out + 48);
+    st_fq(p.y.c0, out + 96);
+    st_fq(p.y.c1, out + 144);
+  }
+  return r;
+}
+int zgt_g1_in_subgroup(const uint8_t* xy) { return g1_in_subgroup({ld_fq(xy), ld_fq(xy + 48), false}); }
+int zgt_g2_in_subgroup(const uint8_t* xy) {
+  return g2_in_subgroup({{ld_fq(xy), ld_fq(xy + 48)}, {ld_fq(xy + 96), ld_fq(xy + 144)}, false});
+}
+
+// miller loop of affine P (x||y) and Q (x0||x1||y0||y1), conjugated
+void zgt_miller(const uint8_t* p, const uint8_t* q, uint8_t* out) {
+  G1A P = {ld_fq(p), ld_fq(p + 48), false};
+  G2A Q = {{ld_fq(q), ld_fq(q + 48)}, {ld_fq(q + 96), ld_fq(q + 144)}, false};
+  f12_to_bytes(miller_loop_1(P, Q), out);
+}
+
+// prepare a VK from raw uncompressed bytes; returns vk_prepare code; alpha_beta out
+static DevVK g_vk;
+int zgt_vk_prepare(const uint8_t* raw_fields /*96+96+192+192+96+192*/, int n_ic, const uint8_t* ic, uint8_t* ab) {
+  RawVK raw;
+  const uint8_t* p = raw_fields;
+  memcpy(raw.alpha_g1, p, 96); p += 96;
+  memcpy(raw.beta_g1, p, 96); p += 96;
+  memcpy(raw.beta_g2, p, 192); p += 192;
+  memcpy(raw.gamma_g2, p, 192); p += 192;
+  memcpy(raw.delta_g1, p, 96); p += 96;
+  memcpy(raw.delta_g2, p, 192);
+  raw.n_ic = n_ic;
+  for (int i = 0; i < n_ic; i++) memcpy(raw.ic[i], ic + 96 * i, 96);
+  int r = vk_prepare(raw, &g_vk);
+  if (r == 0) f12_to_bytes(g_vk.alpha_beta, ab);
+  return r;
+}
+int zgt_verify_single(const uint8_t* proof, const uint8_t* inputs, int k, uint8_t* gt) {
+  Fq12 g;
+  uint8_t st = verify_single(g_vk, proof, inputs, k, &g);
+  if (st == ST_OK || st == ST_VERIFY_FAILED) f12_to_bytes(g, gt);
+  return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,118 @@
+"""CPU tier: the product's device arithmetic (zebra_amd/csrc/*.h, compiled for the host by
+tests/native) against the oracle (oracle/bls12_381.py)."""
+import random
+
+import pytest
+
+from oracle import bls12_381 as B
+from tests import hostlib
+
+P = B.P
+
+
+@pytest.fixture(scope="module")
+def L():
+    return hostlib.lib()
+
+
+def fq_b(x):
+    return x.to_bytes(48, "big")
+
+
+def rnd_f12(rng):
+    return B.f12_from_coeffs([rng.randrange(P) for _ in range(12)])
+
+
+def test_fq_ops(L):
+    rng = random.Random(1)
+    out = hostlib.buf(48)
+    for _ in range(200):
+        a, b = rng.randrange(P), rng.randrange(P)
+        for fn, want in ((L.zgt_fq_mul, a * b % P), (L.zgt_fq_add, (a + b) % P), (L.zgt_fq_sub, (a - b) % P)):
+            fn(fq_b(a), fq_b(b), out)
+            assert int.from_bytes(out.raw, "big") == want
+    for a in (1, 2, P - 1, rng.randrange(P)):
+        L.zgt_fq_inv(fq_b(a), out)
+        assert int.from_bytes(out.raw, "big") * a % P == 1
+        ok = L.zgt_fq_sqrt(fq_b(a), out)
+        assert bool(ok) == (B.fq_sqrt(a) is not None)
+        if ok:
+            assert pow(int.from_bytes(out.raw, "big"), 2, P) == a
+
+
+def test_fr_mul(L):
+    rng = random.Random(2)
+    out = hostlib.buf(32)
+    for _ in range(100):
+        a, b = rng.randrange(B.R), rng.randrange(B.R)
+        L.zgt_fr_mul(a.to_bytes(32, "little"), b.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw, "little") == a * b % B.R
+
+
+def test_f12_ops(L):
+    rng = random.Random(3)
+    out = hostlib.buf(576)
+    for _ in range(5):
+        a, b = rnd_f12(rng), rnd_f12(rng)
+        L.zgt_f12_mul(B.f12_to_bytes(a), B.f12_to_bytes(b), out)
+        assert out.raw == B.f12_to_bytes(B.f12_mul(a, b))
+        L.zgt_f12_sqr(B.f12_to_bytes(a), out)
+        assert out.raw == B.f12_to_bytes(B.f12_sqr(a))
+        L.zgt_f12_inv(B.f12_to_bytes(a), out)
+        assert out.raw == B.f12_to_bytes(B.f12_inv(a))
+        for k in (1, 2, 3):
+            L.zgt_f12_frob(B.f12_to_bytes(a), k, out)
+            assert out.raw == B.f12_to_bytes(B.f12_frob(a, k))
+
+
+def test_f2_sqrt(L):
+    rng = random.Random(4)
+    out = hostlib.buf(96)
+    for _ in range(6):
+        a = (rng.randrange(P), rng.randrange(P))
+        ok = L.zgt_f2_sqrt(fq_b(a[0]) + fq_b(a[1]), out)
+        want = B.f2_sqrt(a)
+        assert bool(ok) == (want is not None)
+        if ok:
+            s = (int.from_bytes(out.raw[:48], "big"), int.from_bytes(out.raw[48:], "big"))
+            assert B.f2_sqr(s) == a
+
+
+def test_final_exp_and_miller(L):
+    rng = random.Random(5)
+    out = hostlib.buf(576)
+    f = rnd_f12(rng)
+    L.zgt_final_exp(B.f12_to_bytes(f), out)
+    assert out.raw == B.f12_to_bytes(B.final_exponentiation(f))
+    p = B.ec_mul(B.FQ, B.G1_GEN, 12345)
+    q = B.ec_mul(B.FQ2, B.G2_GEN, 678)
+    L.zgt_miller(fq_b(p[0]) + fq_b(p[1]), b"".join(fq_b(v) for v in (q[0][0], q[0][1], q[1][0], q[1][1])), out)
+    assert out.raw == B.f12_to_bytes(B.miller_loop([(p, B.g2_prepare(q))]))
+
+
+def test_subgroup_checks(L):
+    rng = random.Random(6)
+    out = hostlib.buf(192)
+    # in-subgroup points
+    for k in (1, 7, rng.randrange(B.R)):
+        p = B.ec_mul(B.FQ, B.G1_GEN, k)
+        assert L.zgt_g1_in_subgroup(fq_b(p[0]) + fq_b(p[1])) == 1
+        q = B.ec_mul(B.FQ2, B.G2_GEN, k)
+        assert L.zgt_g2_in_subgroup(b"".join(fq_b(v) for v in (q[0][0], q[0][1], q[1][0], q[1][1]))) == 1
+    # random on-curve points: compare with the oracle's naive [r]P check
+    n1 = n2 = 0
+    while n1 < 6:
+        x = rng.randrange(P)
+        y = B.fq_sqrt((x ** 3 + 4) % P)
+        if y is None:
+            continue
+        n1 += 1
+        assert L.zgt_g1_in_subgroup(fq_b(x) + fq_b(y)) == int(B.g1_in_subgroup((x, y)))
+    while n2 < 3:
+        x = (rng.randrange(P), rng.randrange(P))
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(x), x), B.B2))
+        if y is None:
+            continue
+        n2 += 1
+        assert L.zgt_g2_in_subgroup(b"".join(fq_b(v) for v in (x[0], x[1], y[0], y[1]))) == int(
+            B.g2_in_subgroup((x, y)))

@@ -1,0 +1,362 @@
+// zg_field.h -- BLS12-381 prime fields for gfx950: Fq (381-bit, 12 x 32-bit limbs) and
+// Fr (255-bit, 8 x 32-bit limbs), Montgomery form (R = 2^384 / 2^256).
+//
+// Restates the arithmetic of pairing 0.14.2 `bls12_381::{Fq, Fr}` (6/4 x 64-bit limbs
+// there) in the limb width CDNA4's VALU multiplies natively:
+// every 32x32->64 product + 64-bit addend is one v_mad_u64_u32. MFMA is not used.
+//
+// Montgomery multiplication is the "no-carry" CIOS form: both moduli have a top limb
+// below 2^31 - 1, so the running accumulator never needs an (N+1)-th word.
+//
+// Functions are __host__ __device__ so tests/native can execute the identical code on
+// the CPU (test harness only; the product path launches it on the GPU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "zg_constants.h"
+
+#define ZG_HD __host__ __device__
+#define ZG_INL __host__ __device__ __forceinline__
+#define ZG_NOINL __host__ __device__ __attribute__((noinline))
+
+namespace zg {
+
+struct FqM {
+  static constexpr int N = 12;
+  static constexpr uint32_t INV = FQ_INV;
+  ZG_INL static uint32_t p(int i) { return FQ_P[i]; }
+};
+struct FrM {
+  static constexpr int N = 8;
+  static constexpr uint32_t INV = FR_INV;
+  ZG_INL static uint32_t p(int i) { return FR_R[i]; }
+};
+
+template <class M>
+struct Fp {
+  uint32_t l[M::N];
+};
+using Fq = Fp<FqM>;
+using Fr = Fp<FrM>;
+
+template <class M>
+ZG_INL Fp<M> fp_zero() {
+  Fp<M> r;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) r.l[i] = 0;
+  return r;
+}
+
+ZG_INL Fq fq_one() {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = FQ_ONE[i];
+  return r;
+}
+ZG_INL Fr fr_one() {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = FR_ONE[i];
+  return r;
+}
+ZG_INL Fq fq_const(const uint32_t* c) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = c[i];
+  return r;
+}
+
+template <class M>
+ZG_INL bool fp_is_zero(const Fp<M>& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) acc |= a.l[i];
+  return acc == 0;
+}
+
+template <class M>
+ZG_INL bool fp_eq(const Fp<M>& a, const Fp<M>& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) acc |= a.l[i] ^ b.l[i];
+  return acc == 0;
+}
+
+// r = a - p if a >= p else a   (a < 2p)
+template <class M>
+ZG_INL Fp<M> fp_reduce_once(const Fp<M>& a) {
+  Fp<M> d;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)a.l[i] - M::p(i) - borrow;
+    d.l[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  Fp<M> r;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) r.l[i] = borrow ? a.l[i] : d.l[i];
+  return r;
+}
+
+template <class M>
+ZG_INL Fp<M> fp_add(const Fp<M>& a, const Fp<M>& b) {
+  Fp<M> s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)a.l[i] + b.l[i] + c;
+    s.l[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return fp_reduce_once<M>(s);
+}
+
+template <class M>
+ZG_INL Fp<M> fp_sub(const Fp<M>& a, const Fp<M>& b) {
+  Fp<M> d;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)a.l[i] - b.l[i] - borrow;
+    d.l[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  // add back p masked by borrow
+  uint32_t mask = 0u - borrow;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)d.l[i] + (M::p(i) & mask) + c;
+    d.l[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return d;
+}
+
+template <class M>
+ZG_INL Fp<M> fp_neg(const Fp<M>& a) {
+  return fp_sub<M>(fp_zero<M>(), a);
+}
+
+template <class M>
+ZG_INL Fp<M> fp_dbl(const Fp<M>& a) {
+  return fp_add<M>(a, a);
+}
+
+// Montgomery product, no-carry CIOS. a, b < p  ->  result < p.
+template <class M>
+ZG_INL Fp<M> fp_mul_inl(const Fp<M>& a, const Fp<M>& b) {
+  constexpr int N = M::N;
+  uint32_t t[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint32_t bi = b.l[i];
+    uint64_t A = (uint64_t)a.l[0] * bi + t[0];
+    t[0] = (uint32_t)A;
+    A >>= 32;
+    const uint32_t m = t[0] * M::INV;
+    uint64_t C = ((uint64_t)m * M::p(0) + t[0]) >> 32;
+#pragma unroll
+    for (int j = 1; j < N; j++) {
+      A = (uint64_t)a.l[j] * bi + t[j] + A;
+      t[j] = (uint32_t)A;
+      A >>= 32;
+      C = (uint64_t)m * M::p(j) + t[j] + C;
+      t[j - 1] = (uint32_t)C;
+      C >>= 32;
+    }
+    t[N - 1] = (uint32_t)(C + A);
+  }
+  Fp<M> r;
+#pragma unroll
+  for (int j = 0; j < N; j++) r.l[j] = t[j];
+  return fp_reduce_once<M>(r);
+}
+
+// Out-of-line multiply: the tower above calls this ~54x per Fq12 product; inlining all of
+// them would blow the instruction cache. Operands cross the call as ext_vector values so
+// the AMDGPU calling convention keeps them in VGPRs (a by-value aggregate of 12 dwords
+// would go through scratch).
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+ZG_NOINL inline u32x16 fq_mul_v(u32x8 a0, u32x4 a1, u32x8 b0, u32x4 b1) {
+  Fq a, b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.l[i] = a0[i];
+    b.l[i] = b0[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    a.l[8 + i] = a1[i];
+    b.l[8 + i] = b1[i];
+  }
+  Fq r = fp_mul_inl<FqM>(a, b);
+  u32x16 o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o[i] = r.l[i];
+  o[12] = o[13] = o[14] = o[15] = 0;
+  return o;
+}
+ZG_INL Fq fq_mul(const Fq& a, const Fq& b) {
+  u32x8 a0, b0;
+  u32x4 a1, b1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a0[i] = a.l[i];
+    b0[i] = b.l[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    a1[i] = a.l[8 + i];
+    b1[i] = b.l[8 + i];
+  }
+  u32x16 o = fq_mul_v(a0, a1, b0, b1);
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = o[i];
+  return r;
+}
+ZG_NOINL inline u32x8 fr_mul_v(u32x8 a0, u32x8 b0) {
+  Fr a, b;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.l[i] = a0[i];
+    b.l[i] = b0[i];
+  }
+  Fr r = fp_mul_inl<FrM>(a, b);
+  u32x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o[i] = r.l[i];
+  return o;
+}
+ZG_INL Fr fr_mul(const Fr& a, const Fr& b) {
+  u32x8 a0, b0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a0[i] = a.l[i];
+    b0[i] = b.l[i];
+  }
+  u32x8 o = fr_mul_v(a0, b0);
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = o[i];
+  return r;
+}
+
+ZG_INL Fq fq_sqr(const Fq& a) { return fq_mul(a, a); }
+ZG_INL Fq fq_add(const Fq& a, const Fq& b) { return fp_add<FqM>(a, b); }
+ZG_INL Fq fq_sub(const Fq& a, const Fq& b) { return fp_sub<FqM>(a, b); }
+ZG_INL Fq fq_neg(const Fq& a) { return fp_neg<FqM>(a); }
+ZG_INL Fq fq_dbl(const Fq& a) { return fp_add<FqM>(a, a); }
+ZG_INL bool fq_is_zero(const Fq& a) { return fp_is_zero<FqM>(a); }
+ZG_INL bool fq_eq(const Fq& a, const Fq& b) { return fp_eq<FqM>(a, b); }
+ZG_INL Fr fr_add(const Fr& a, const Fr& b) { return fp_add<FrM>(a, b); }
+
+// a^e for an exponent given as little-endian limbs (square-and-multiply, MSB first).
+ZG_NOINL inline void fq_pow_limbs_p(Fq* out, const Fq* a, const uint32_t* e, int nbits) {
+  Fq r = fq_one();
+  const Fq base = *a;
+  for (int i = nbits - 1; i >= 0; i--) {
+    r = fq_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fq_mul(r, base);
+  }
+  *out = r;
+}
+ZG_INL Fq fq_pow_limbs(const Fq& a, const uint32_t* e, int nbits) {
+  Fq r;
+  fq_pow_limbs_p(&r, &a, e, nbits);
+  return r;
+}
+
+ZG_INL Fq fq_inv(const Fq& a) { return fq_pow_limbs(a, FQ_EXP_INV, 381); }
+
+// Returns true and sets *out if a is a square (pairing Fq::sqrt: p = 3 mod 4).
+ZG_INL bool fq_sqrt(const Fq& a, Fq* out) {
+  Fq s = fq_pow_limbs(a, FQ_EXP_SQRT, 380);
+  *out = s;
+  return fq_eq(fq_sqr(s), a);
+}
+
+// canonical (non-Montgomery) limbs <-> Montgomery
+ZG_INL Fq fq_to_mont(const Fq& a) { return fq_mul(a, fq_const(FQ_R2)); }
+ZG_INL Fq fq_from_mont(const Fq& a) {
+  Fq one;
+#pragma unroll
+  for (int i = 0; i < 12; i++) one.l[i] = i == 0 ? 1u : 0u;
+  return fq_mul(a, one);
+}
+
+// Compare canonical integers (non-Montgomery limbs): a > b
+template <class M>
+ZG_INL bool fp_gt_canon(const Fp<M>& a, const Fp<M>& b) {
+  // a > b  <=>  b - a borrows
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)b.l[i] - a.l[i] - borrow;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return borrow != 0;
+}
+
+// canonical limbs < modulus ?
+template <class M>
+ZG_INL bool fp_lt_modulus(const Fp<M>& a) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < M::N; i++) {
+    uint64_t t = (uint64_t)a.l[i] - M::p(i) - borrow;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return borrow != 0;
+}
+
+// 48 big-endian bytes -> canonical limbs
+ZG_INL Fq fq_limbs_from_be(const uint8_t* b) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  return r;
+}
+ZG_INL void fq_limbs_to_be(const Fq& a, uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.l[i] >> 24);
+    q[1] = (uint8_t)(a.l[i] >> 16);
+    q[2] = (uint8_t)(a.l[i] >> 8);
+    q[3] = (uint8_t)a.l[i];
+  }
+}
+// 32 little-endian bytes -> canonical Fr limbs
+ZG_INL Fr fr_limbs_from_le(const uint8_t* b) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    r.l[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+             ((uint32_t)b[4 * i + 3] << 24);
+  return r;
+}
+ZG_INL Fr fr_to_mont(const Fr& a) {
+  Fr r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.l[i] = FR_R2[i];
+  return fr_mul(a, r2);
+}
+ZG_INL Fr fr_from_mont(const Fr& a) {
+  Fr one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.l[i] = i == 0 ? 1u : 0u;
+  return fr_mul(a, one);
+}
+
+}  // namespace zg

@@ -1,0 +1,117 @@
+// zg_groth16.h -- bellman 0.1.0 groth16 semantics on gfx950 (per-thread building blocks).
+//
+//   Proof::<Bls12>::read   (called at verification/src/sapling.rs:158,203,
+//                           crypto/src/groth16.rs:54)        -> proof_decode_point
+//   prepare_verifying_key  (crypto/src/json/groth16.rs:14,21,27) -> vk_prepare
+//   verify_proof           (verification/src/sapling.rs:162,207, sprout.rs:73-77)
+//                                                            -> verify_single
+// SURVEY.md 8(a) rows a1-a4, a8.
+#pragma once
+#include "zg_pairing.h"
+
+namespace zg {
+
+enum : uint8_t {
+  ST_OK = 0,
+  ST_DECODE_INVALID = 1,
+  ST_MALFORMED_VK = 2,
+  ST_VERIFY_FAILED = 3,
+  ST_INPUT_NONCANONICAL = 4,
+  ST_PENDING = 255,
+};
+
+#define ZG_MAX_IC 10
+#define ZG_MAX_INPUTS 9
+#define ZG_NKINDS 3
+
+// A prepared verifying key, resident in HBM.
+struct DevVK {
+  int loaded;
+  int ic_len;
+  G1A alpha;
+  G2A beta, gamma, delta;
+  G1A ic[ZG_MAX_IC];
+  Fq12 alpha_beta;                 // alpha_g1_beta_g2 (final-exponentiated)
+  Line neg_gamma_lines[ZG_NCOEFF]; // G2Prepared(-gamma)
+  Line neg_delta_lines[ZG_NCOEFF]; // G2Prepared(-delta)
+  Line beta_lines[ZG_NCOEFF];      // G2Prepared(beta)  (batch alpha/beta term)
+};
+
+// Raw uncompressed VK as uploaded by the host (crypto/src/json/groth16.rs:33-49 fields).
+struct RawVK {
+  uint8_t alpha_g1[96], beta_g1[96], beta_g2[192], gamma_g2[192], delta_g1[96], delta_g2[192];
+  uint8_t ic[ZG_MAX_IC][96];
+  int n_ic;
+};
+
+// prepare_verifying_key. Returns 0 on success, 1 + field index on a decode failure.
+ZG_NOINL inline int vk_prepare(const RawVK& raw, DevVK* vk) {
+  G1A beta_g1, delta_g1;
+  if (g1_decode_uncompressed(raw.alpha_g1, &vk->alpha) == DEC_ERR) return 1;
+  if (g1_decode_uncompressed(raw.beta_g1, &beta_g1) == DEC_ERR) return 2;
+  if (g2_decode_uncompressed(raw.beta_g2, &vk->beta) == DEC_ERR) return 3;
+  if (g2_decode_uncompressed(raw.gamma_g2, &vk->gamma) == DEC_ERR) return 4;
+  if (g1_decode_uncompressed(raw.delta_g1, &delta_g1) == DEC_ERR) return 5;
+  if (g2_decode_uncompressed(raw.delta_g2, &vk->delta) == DEC_ERR) return 6;
+  for (int i = 0; i < raw.n_ic; i++)
+    if (g1_decode_uncompressed(raw.ic[i], &vk->ic[i]) == DEC_ERR) return 7 + i;
+  vk->ic_len = raw.n_ic;
+  // E::pairing(alpha, beta): miller_loop skips infinity pairs -> f = 1 -> FE(1) = 1
+  if (!vk->alpha.inf && !vk->beta.inf)
+    vk->alpha_beta = final_exponentiation(miller_loop_1(vk->alpha, vk->beta));
+  else
+    vk->alpha_beta = f12_one();
+  G2A ng = vk->gamma, nd = vk->delta;
+  ng.y = f2_neg(ng.y);
+  nd.y = f2_neg(nd.y);
+  if (!ng.inf) g2_prepare(ng, vk->neg_gamma_lines);
+  if (!nd.inf) g2_prepare(nd, vk->neg_delta_lines);
+  if (!vk->beta.inf) g2_prepare(vk->beta, vk->beta_lines);
+  vk->loaded = 1;
+  return 0;
+}
+
+// Decode A || B || C (192 B) with bellman's rules: every point subgroup-checked and the
+// point at infinity rejected. Returns true on success.
+ZG_INL bool proof_decode(const uint8_t* pb, G1A* a, G2A* b, G1A* c) {
+  if (g1_decompress(pb, a) != DEC_OK) return false;
+  if (g2_decompress(pb + 48, b) != DEC_OK) return false;
+  if (g1_decompress(pb + 144, c) != DEC_OK) return false;
+  return true;
+}
+
+// 32-byte LE inputs -> canonical Fr limbs; false if any is >= r
+ZG_INL bool inputs_canonical(const uint8_t* in, int k, Fr* x) {
+  bool ok = true;
+  for (int j = 0; j < k; j++) {
+    x[j] = fr_limbs_from_le(in + 32 * j);
+    ok = ok && fp_lt_modulus<FrM>(x[j]);
+  }
+  return ok;
+}
+
+// acc = ic[0] + sum_j x_j ic[j+1]  (bellman verify_proof; canonical scalars)
+ZG_NOINL inline G1J compute_acc(const DevVK& vk, const Fr* x, int k) {
+  G1J acc = jac_from_aff(vk.ic[0]);
+  for (int j = 0; j < k; j++) acc = jac_add(acc, jac_mul_limbs(vk.ic[j + 1], x[j].l, 255));
+  return acc;
+}
+
+// bellman verify_proof for one proof: status and the final-exponentiated left-hand side
+// final_exponentiation(miller_loop([(A, B), (acc, -gamma), (C, -delta)])).
+ZG_NOINL inline uint8_t verify_single(const DevVK& vk, const uint8_t* pb, const uint8_t* in, int k, Fq12* gt) {
+  Fr x[ZG_MAX_INPUTS];
+  if (!inputs_canonical(in, k, x)) return ST_INPUT_NONCANONICAL;
+  G1A a, c;
+  G2A b;
+  if (!proof_decode(pb, &a, &b, &c)) return ST_DECODE_INVALID;
+  if (k + 1 != vk.ic_len) return ST_MALFORMED_VK;
+  G1A acc = jac_to_aff(compute_acc(vk, x, k));
+  Fq12 f = miller_loop_1(a, b);
+  if (!acc.inf && !vk.gamma.inf) f = f12_mul(f, miller_loop_prepared(acc, vk.neg_gamma_lines));
+  if (!vk.delta.inf) f = f12_mul(f, miller_loop_prepared(c, vk.neg_delta_lines));
+  *gt = final_exponentiation(f);
+  return f12_eq(*gt, vk.alpha_beta) ? ST_OK : ST_VERIFY_FAILED;
+}
+
+}  // namespace zg
