@@ -1,0 +1,144 @@
+/* zg.h -- C ABI of the MI355X batch Groth16 verifier (BLS12-381) for Zebra's
+ * `verification` crate. Plain pointers and sizes; caller-owned buffers only; no
+ * allocation crosses the ABI.
+ *
+ * Reference interfaces replaced (defuse/zebra @ 2025-01-12, bellman 0.1.0, pairing 0.14.2):
+ *   zg_vk_load_builtin / zg_vk_load_json   <- crypto::load_sapling_spend_verifying_key,
+ *        load_sapling_output_verifying_key, load_joinsplit_groth16_verifying_key
+ *        (crypto/src/json/groth16.rs:11-28) + bellman::groth16::prepare_verifying_key
+ *        (called at crypto/src/json/groth16.rs:14,21,27); statics network/src/consensus.rs:4-11
+ *   zg_vk_load_uncompressed               <- bellman::groth16::VerifyingKey { .. } +
+ *        prepare_verifying_key (as built in verification/src/sapling.rs:345-358)
+ *   zg_verify_one_gt                       <- bellman::groth16::Proof::<Bls12>::read +
+ *        verify_proof for ONE proof (verification/src/sapling.rs:158-167,203-212,
+ *        verification/src/sprout.rs:69-80, crypto/src/groth16.rs:52-56)
+ *   zg_verify_batch                        <- the per-description loops that call the two
+ *        above (sapling.rs:85-94, accept_transaction.rs:575-596) fanned out by rayon
+ *        (verification/src/accept_chain.rs:76-81): one call verifies a whole block /
+ *        import window with per-proof statuses in the reference's error classes.
+ *   zg_batch_* / zg_gt_check               <- (no reference analogue) the 8-GPU split: each
+ *        rank produces one 576-byte Miller partial, gathered over RCCL, one final exp.
+ *
+ * Threading: calls on different contexts are independent; one call at a time per
+ * context (internal mutex). Every context owns its HIP stream and device buffers.
+ */
+#ifndef ZG_H
+#define ZG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* proof kinds == verifying keys */
+#define ZG_KIND_SPEND 0  /* res/sapling-spend-verifying-key.json, 7 public inputs */
+#define ZG_KIND_OUTPUT 1 /* res/sapling-output-verifying-key.json, 5 public inputs */
+#define ZG_KIND_SPROUT 2 /* res/sprout-groth16-key.json, 9 public inputs */
+
+/* per-proof status (reference error class in brackets) */
+#define ZG_STATUS_OK 0             /* verify_proof == Ok(true) */
+#define ZG_STATUS_DECODE_INVALID 1 /* Proof::read -> io::Error(InvalidData): ProofError::Invalid /
+                                      sprout ErrorKind::InvalidEncoding */
+#define ZG_STATUS_MALFORMED_VK 2   /* SynthesisError::MalformedVerifyingKey: ProofError::Synthesis /
+                                      InvalidGrothProof */
+#define ZG_STATUS_VERIFY_FAILED 3  /* verify_proof == Ok(false): ProofError::Failed /
+                                      InvalidGrothProof */
+#define ZG_STATUS_INPUT_NONCANONICAL 4 /* a public input >= r (unreachable from the reference,
+                                          whose Fr are always reduced) */
+
+/* return codes */
+#define ZG_OK 0
+#define ZG_E_INVAL (-1)   /* bad argument */
+#define ZG_E_HIP (-2)     /* HIP runtime / device error */
+#define ZG_E_NOVK (-3)    /* a proof refers to a kind whose VK is not loaded */
+#define ZG_E_VK (-4)      /* VK JSON/points failed to decode (crypto/src/json/groth16.rs:88-99) */
+#define ZG_E_NOMEM (-5)   /* batch larger than max_batch / allocation failure */
+#define ZG_E_STATE (-6)   /* batch API called out of order */
+
+#define ZG_PROOF_BYTES 192
+#define ZG_FR_BYTES 32
+#define ZG_MAX_INPUTS 9
+#define ZG_INPUT_STRIDE (ZG_MAX_INPUTS * ZG_FR_BYTES) /* 288 B per proof, unused slots ignored */
+#define ZG_GT_BYTES 576 /* Fq12: 12 x 48-byte big-endian canonical coefficients, tower order */
+#define ZG_R_BYTES 16   /* batch scalar r_i: 128-bit little-endian, non-zero */
+
+typedef struct zg_config {
+  int device;         /* HIP device ordinal (one process per GPU) */
+  uint32_t max_batch; /* capacity of one batch (proofs); 0 -> 65536 */
+  int seeded;         /* 1: batch scalars r_i from BLAKE2b(seed, i) (tests); 0: OS RNG */
+  uint64_t seed;
+} zg_config;
+
+typedef struct zg_ctx zg_ctx;
+
+zg_ctx* zg_create(const zg_config* cfg);
+void zg_destroy(zg_ctx* ctx);
+const char* zg_last_error(zg_ctx* ctx);
+/* library build tag (architecture + version), static string */
+const char* zg_version(void);
+
+/* ---- verifying keys (prepared once per process, resident in HBM) */
+int zg_vk_load_builtin(zg_ctx* ctx, int kind);
+int zg_vk_load_json(zg_ctx* ctx, int kind, const char* json, size_t len);
+int zg_vk_load_uncompressed(zg_ctx* ctx, int kind, const uint8_t alpha_g1[96], const uint8_t beta_g1[96],
+                            const uint8_t beta_g2[192], const uint8_t gamma_g2[192],
+                            const uint8_t delta_g1[96], const uint8_t delta_g2[192], size_t n_ic,
+                            const uint8_t* ic /* n_ic x 96 */);
+/* the prepared alpha_g1_beta_g2 (GT) of a loaded VK */
+int zg_vk_alpha_beta(zg_ctx* ctx, int kind, uint8_t gt[ZG_GT_BYTES]);
+
+/* ---- one proof, bellman-exact: status and, for OK / VERIFY_FAILED, the final-exponentiated
+ * left-hand side  FE(ML(A,B) * ML(acc,-gamma) * ML(C,-delta))  (== alpha_g1_beta_g2 iff OK) */
+int zg_verify_one_gt(zg_ctx* ctx, int kind, const uint8_t proof[ZG_PROOF_BYTES], const uint8_t* inputs,
+                     size_t n_inputs, uint8_t* status, uint8_t gt[ZG_GT_BYTES]);
+
+/* ---- n proofs, each verified on its own exactly like bellman verify_proof (no batch
+ * randomness): one GPU thread per proof. Same layouts as zg_verify_batch; gts optional
+ * (n x 576, written for OK / VERIFY_FAILED). */
+int zg_verify_each(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds, const uint8_t* inputs,
+                   const uint8_t* n_inputs, uint8_t* status, uint8_t* gts);
+
+/* ---- a batch of n proofs (host buffers).
+ *   proofs   n x 192 B (A || B || C compressed)
+ *   kinds    n x ZG_KIND_*
+ *   inputs   n x ZG_INPUT_STRIDE (canonical little-endian Fr; slots past k ignored)
+ *   n_inputs optional n x count (NULL: 7 / 5 / 9 by kind); count + 1 != |ic| -> MALFORMED_VK
+ *   r        optional n x 16 B batch scalars (NULL: generated per zg_config)
+ *   status   out, n bytes (ZG_STATUS_*), exact per proof (bisection on failure)
+ *   gt_out   optional out: prod_i LHS_i^{r_i} over proofs that decoded with a well-formed VK
+ */
+int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds, const uint8_t* inputs,
+                    const uint8_t* n_inputs, const uint8_t* r, uint8_t* status, uint8_t* gt_out);
+
+/* ---- split form for multi-GPU (one process per GPU):
+ *   zg_batch_begin[_device]  decode + batch algebra + Miller loops + product trees
+ *   zg_batch_partial         this rank's Miller partial F_g (576 B, not final-exponentiated)
+ *   zg_gt_check              product of `count` partials, ONE final exponentiation, == 1 ?
+ *   zg_batch_finish          statuses; when batch_ok == 0 bisects this rank's shard
+ * The *_device variant takes device pointers (HBM-resident inputs; same layouts). */
+int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds, const uint8_t* inputs,
+                   const uint8_t* n_inputs, const uint8_t* r);
+int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,
+                          const void* d_inputs, const void* d_n_inputs, const void* d_r);
+int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
+int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
+int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);
+
+/* ---- synthetic workload (bench/tests): Groth16 re-randomization of real proofs,
+ * out[i] = rerandomize(src[src_index[i]]) with (t, s) = BLAKE2b-512("zg-rerand"||seed||i)
+ * (A,B,C) -> (t^-1 A, t B + t s delta, C + s A); valid iff the source is. */
+int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, const uint8_t* src_kinds,
+                         size_t n, const uint32_t* src_index, uint64_t seed, uint8_t* out_proofs);
+
+/* ---- measurement helpers */
+/* time (ms, HIP events on the context stream) of the most recent zg_batch_begin* phases:
+ * [0] decode+scalar, [1] miller, [2] product tree, [3] root check (partial) */
+int zg_last_timings(zg_ctx* ctx, float* ms4);
+/* microbenchmark: v_mad_u64_u32 chains; returns achieved 32x32->64 MACs per second */
+int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

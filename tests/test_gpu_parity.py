@@ -1,0 +1,161 @@
+"""GPU tier (MI355X): the HIP path through the C ABI against the golden fixtures (oracle
+outputs on the reference's own proofs) and size-independent properties at larger sizes.
+Bar: bit-exact statuses and GT bytes."""
+import pytest
+
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+KN = {0: "spend", 1: "output", 2: "sprout"}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zebra_amd import Context
+    c = Context(device=0, max_batch=8192, seed=7)
+    yield c
+    c.close()
+
+
+def fx_batch(items):
+    from zebra_amd import pack_inputs
+    proofs = b"".join(bytes.fromhex(e["proof"]) for e in items)
+    kinds = bytes(e["kind"] for e in items)
+    inputs = pack_inputs([[bytes.fromhex(x) for x in e["inputs"]] for e in items])
+    nin = bytes(len(e["inputs"]) for e in items)
+    return proofs, kinds, inputs, nin
+
+
+def test_library_is_gfx950_hip():
+    from zebra_amd import zg
+    assert b"gfx950" in zg.lib().zg_version()
+
+
+def test_mad_rate_probe(ctx):
+    rate = ctx.bench_mad_rate()
+    assert rate > 1e12, rate
+
+
+def test_alpha_beta(ctx):
+    vk = load_golden("vk.json")
+    for k, name in KN.items():
+        assert ctx.alpha_beta(k).hex() == vk[name]["alpha_g1_beta_g2"]
+
+
+def test_verify_one_gt_real(ctx):
+    for e in load_golden("real_proofs.json")["proofs"]:
+        st, gt = ctx.verify_one_gt(e["kind"], bytes.fromhex(e["proof"]), [bytes.fromhex(x) for x in e["inputs"]])
+        assert st == 0, e["name"]
+        assert gt.hex() == e["lhs_gt"], e["name"]
+
+
+def test_verify_each_real_and_mutants(ctx):
+    items = load_golden("real_proofs.json")["proofs"] + [
+        m for m in load_golden("mutants.json")["mutants"] if m["vk"] == "builtin"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    sts, gts = ctx.verify_each(proofs, kinds, inputs, nin)
+    for e, st, gt in zip(items, sts, gts):
+        assert st == e["status"], e.get("name")
+        if e.get("lhs_gt"):
+            assert gt.hex() == e["lhs_gt"], e.get("name")
+
+
+def test_bad_vk_malformed(ctx):
+    """verification/src/sapling.rs:428-432: an empty-ic VK -> Proof(Synthesis)."""
+    from zebra_amd import Context
+    c = Context(device=0, max_batch=64, load_builtin=False)
+    g1 = bytes([0x40]) + bytes(95)
+    g2 = bytes([0x40]) + bytes(191)
+    c.vk_load_uncompressed(0, g1, g1, g2, g2, g1, g2, [])
+    e = load_golden("real_proofs.json")["proofs"][0]
+    st, _ = c.verify_one_gt(0, bytes.fromhex(e["proof"]), [bytes.fromhex(x) for x in e["inputs"]])
+    assert st == 2
+    c.close()
+
+
+def test_rerandomize_matches_oracle(ctx):
+    b = load_golden("batch64.json")
+    real = {e["name"]: e for e in load_golden("real_proofs.json")["proofs"]}
+    srcs = ["S1", "S2", "O1", "O2", "O3", "J1", "J2", "J3", "J4"]
+    src_proofs = b"".join(bytes.fromhex(real[s]["proof"]) for s in srcs)
+    src_kinds = bytes(real[s]["kind"] for s in srcs)
+    out = ctx.synth_rerandomize(src_proofs, src_kinds, [i % 9 for i in range(64)], b["seed"])
+    for i, it in enumerate(b["items"]):
+        if it["corruption"] in (None, "input0_plus1"):
+            assert out[192 * i:192 * (i + 1)].hex() == it["proof"], i
+
+
+def test_batch64_statuses_and_gt(ctx):
+    b = load_golden("batch64.json")
+    items = b["items"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    r = b"".join(bytes.fromhex(e["r"]) for e in items)
+    sts, gt = ctx.verify_batch(proofs, kinds, inputs, nin, r=r, want_gt=True)
+    assert sts == [e["status"] for e in items]
+    assert gt.hex() == b["gt_out"]
+
+
+def test_batch_all_valid_real(ctx):
+    items = load_golden("real_proofs.json")["proofs"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    sts, _ = ctx.verify_batch(proofs, kinds, inputs, nin)
+    assert sts == [0] * len(items)
+
+
+def test_split_partials(ctx):
+    """two shards -> two 576-byte partials -> one final exponentiation (the RCCL path's math)."""
+    b = load_golden("batch64.json")
+    good = [e for e in b["items"] if e["status"] == 0]
+    parts = []
+    for shard in (good[:20], good[20:]):
+        proofs, kinds, inputs, nin = fx_batch(shard)
+        ctx.batch_begin(proofs, kinds, inputs, nin)
+        parts.append(ctx.batch_partial())
+        assert ctx.batch_finish(True, len(shard)) == [0] * len(shard)
+    assert ctx.gt_check(parts)
+    bad = [e for e in b["items"] if e["status"] == 3]
+    proofs, kinds, inputs, nin = fx_batch(bad + good[:5])
+    ctx.batch_begin(proofs, kinds, inputs, nin)
+    p2 = ctx.batch_partial()
+    assert not ctx.gt_check([parts[0], p2])
+    assert ctx.batch_finish(False, len(bad) + 5) == [3] * len(bad) + [0] * 5
+
+
+def test_batch_4096_one_percent_corrupted(ctx):
+    """config 4 shape: 4,096 re-randomized proofs, 41 corrupted -> exact reject set."""
+    import random
+    from zebra_amd import pack_inputs
+    real = load_golden("real_proofs.json")["proofs"]
+    pts = load_golden("points.json")
+    n = 4096
+    src_proofs = b"".join(bytes.fromhex(e["proof"]) for e in real)
+    src_kinds = bytes(e["kind"] for e in real)
+    idx = [i % len(real) for i in range(n)]
+    proofs = bytearray(ctx.synth_rerandomize(src_proofs, src_kinds, idx, 3))
+    rows = [[bytes.fromhex(x) for x in real[j]["inputs"]] for j in idx]
+    rng = random.Random(3)
+    bad = sorted(rng.sample(range(n), 41))
+    want = [0] * n
+    for q, i in enumerate(bad):
+        kind = q % 5
+        if kind == 0:     # public-input tweak -> VERIFY_FAILED
+            x = bytearray(rows[i][0])
+            x[0] ^= 1
+            rows[i] = [bytes(x)] + rows[i][1:]
+            want[i] = 3
+        elif kind == 1:   # A <-> C swap -> VERIFY_FAILED
+            p = proofs[192 * i:192 * i + 192]
+            proofs[192 * i:192 * i + 192] = p[144:] + p[48:144] + p[:48]
+            want[i] = 3
+        elif kind == 2:   # compression flag cleared -> DECODE_INVALID
+            proofs[192 * i] &= 0x7F
+            want[i] = 1
+        elif kind == 3:   # non-subgroup G2 B -> DECODE_INVALID
+            proofs[192 * i + 48:192 * i + 144] = bytes.fromhex(pts["g2_not_in_subgroup"])
+            want[i] = 1
+        else:             # non-subgroup G1 A -> DECODE_INVALID
+            proofs[192 * i:192 * i + 48] = bytes.fromhex(pts["g1_not_in_subgroup"])
+            want[i] = 1
+    sts, _ = ctx.verify_batch(bytes(proofs), bytes(src_kinds[j] for j in idx), pack_inputs(rows))
+    assert sts == want

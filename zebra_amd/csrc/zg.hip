@@ -1,0 +1,678 @@
+// zg.hip -- host side of the MI355X batch Groth16 verifier: the C ABI of include/zg.h.
+// One translation unit: the kernels (zg_kernels.h) are launched from here on the
+// context's private HIP stream. Everything that touches curve or field arithmetic runs
+// on the GPU; the host parses bytes, drives launches and the bisection, and moves data.
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zg.h"
+#include "zg_blake2b.h"
+#include "zg_kernels.h"
+#include "zg_vk_embed.h"  // generated from zebra_amd/res/*.json by zebra_amd/build.py
+
+using namespace zg;
+
+#define ZG_BLOCK 64
+#define ZG_NODE_CHUNK 4096
+
+struct zg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  uint32_t cap = 0;  // power of two >= max_batch
+  int seeded = 0;
+  uint64_t seed = 0;
+  int vk_loaded[ZG_NKINDS] = {0, 0, 0};
+  int vk_iclen[ZG_NKINDS] = {0, 0, 0};
+  DevVK* d_vk = nullptr;
+  RawVK* d_rawvk = nullptr;
+  int* d_int = nullptr;  // scratch ints
+  // batch
+  uint8_t *d_proofs = nullptr, *d_kinds = nullptr, *d_inputs = nullptr, *d_ninputs = nullptr, *d_r = nullptr,
+          *d_status = nullptr, *d_bytes = nullptr;
+  G1A* d_ptA = nullptr;
+  G2A* d_ptB = nullptr;
+  Fq12* d_ftree = nullptr;
+  G1J* d_ctree = nullptr;
+  Fr* d_stree = nullptr;
+  // node checks
+  int* d_nodes = nullptr;
+  G1J* d_msm = nullptr;
+  Fq12* d_pairf = nullptr;
+  int* d_ok = nullptr;
+  Fq12* d_out = nullptr;
+  // state of the split API
+  int state = 0;
+  size_t n = 0, npad = 0;
+  const uint8_t* cur_ninputs = nullptr;  // device pointer or null
+  hipEvent_t ev[5] = {};
+  float timings[4] = {0, 0, 0, 0};
+  uint64_t calls = 0;
+};
+
+static int fail(zg_ctx* c, int code, const std::string& msg) {
+  c->err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(ctx, ZG_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static unsigned nblocks(size_t n) { return (unsigned)((n + ZG_BLOCK - 1) / ZG_BLOCK); }
+
+extern "C" const char* zg_version(void) { return "zebra_amd zg 0.1 gfx950"; }
+
+extern "C" const char* zg_last_error(zg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+template <class T>
+static hipError_t dalloc(T** p, size_t count) {
+  return hipMalloc((void**)p, sizeof(T) * (count ? count : 1));
+}
+
+extern "C" zg_ctx* zg_create(const zg_config* cfg) {
+  zg_ctx* ctx = new zg_ctx();
+  zg_config def = {0, 65536, 0, 0};
+  if (!cfg) cfg = &def;
+  ctx->device = cfg->device;
+  uint32_t mb = cfg->max_batch ? cfg->max_batch : 65536;
+  uint32_t cap = 1;
+  while (cap < mb) cap <<= 1;
+  ctx->cap = cap;
+  ctx->seeded = cfg->seeded;
+  ctx->seed = cfg->seed;
+  bool ok = hipSetDevice(ctx->device) == hipSuccess && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && dalloc(&ctx->d_vk, ZG_NKINDS) == hipSuccess && dalloc(&ctx->d_rawvk, 1) == hipSuccess &&
+       dalloc(&ctx->d_int, 16) == hipSuccess;
+  ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
+       dalloc(&ctx->d_inputs, (size_t)cap * 288) == hipSuccess && dalloc(&ctx->d_ninputs, cap) == hipSuccess &&
+       dalloc(&ctx->d_r, (size_t)cap * 16) == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
+       dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
+  ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
+       dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
+       dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
+       dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC) == hipSuccess;
+  ok = ok && dalloc(&ctx->d_nodes, ZG_NODE_CHUNK) == hipSuccess &&
+       dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS) == hipSuccess &&
+       dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS) == hipSuccess &&
+       dalloc(&ctx->d_ok, ZG_NODE_CHUNK) == hipSuccess && dalloc(&ctx->d_out, ZG_NODE_CHUNK) == hipSuccess;
+  for (int i = 0; ok && i < 5; i++) ok = hipEventCreate(&ctx->ev[i]) == hipSuccess;
+  ok = ok && hipMemset(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS) == hipSuccess;
+  if (!ok) {
+    zg_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+extern "C" void zg_destroy(zg_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
+                  ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
+                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (int i = 0; i < 5; i++)
+    if (ctx->ev[i]) hipEventDestroy(ctx->ev[i]);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+// ------------------------------------------------------------------ verifying keys
+static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
+  if (kind < 0 || kind >= ZG_NKINDS) return fail(ctx, ZG_E_INVAL, "bad kind");
+  if (raw.n_ic > ZG_MAX_IC) return fail(ctx, ZG_E_INVAL, "ic longer than 10");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(ctx->d_rawvk, &raw, sizeof(RawVK), hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_vk_prepare, dim3(1), dim3(1), 0, ctx->stream, ctx->d_rawvk, ctx->d_vk + kind, ctx->d_int);
+  HIPCHK(hipGetLastError());
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, ctx->d_int, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (err) {
+    int z = 0;
+    hipMemcpy(&ctx->d_vk[kind].loaded, &z, sizeof(int), hipMemcpyHostToDevice);
+    ctx->vk_loaded[kind] = 0;
+    return fail(ctx, ZG_E_VK, "Invalid curve point in verifying key (field " + std::to_string(err) + ")");
+  }
+  ctx->vk_loaded[kind] = 1;
+  ctx->vk_iclen[kind] = raw.n_ic;
+  return ZG_OK;
+}
+
+extern "C" int zg_vk_load_uncompressed(zg_ctx* ctx, int kind, const uint8_t alpha_g1[96], const uint8_t beta_g1[96],
+                                       const uint8_t beta_g2[192], const uint8_t gamma_g2[192],
+                                       const uint8_t delta_g1[96], const uint8_t delta_g2[192], size_t n_ic,
+                                       const uint8_t* ic) {
+  if (!ctx) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  RawVK raw;
+  memset(&raw, 0, sizeof(raw));
+  memcpy(raw.alpha_g1, alpha_g1, 96);
+  memcpy(raw.beta_g1, beta_g1, 96);
+  memcpy(raw.beta_g2, beta_g2, 192);
+  memcpy(raw.gamma_g2, gamma_g2, 192);
+  memcpy(raw.delta_g1, delta_g1, 96);
+  memcpy(raw.delta_g2, delta_g2, 192);
+  if (n_ic > ZG_MAX_IC) return fail(ctx, ZG_E_INVAL, "ic longer than 10");
+  raw.n_ic = (int)n_ic;
+  if (n_ic) memcpy(raw.ic, ic, 96 * n_ic);
+  return vk_upload(ctx, kind, raw);
+}
+
+// crypto/src/json/groth16.rs:33-102: serde fields -> hex (optional 0x) of exact length
+static bool json_str_after(const std::string& s, size_t pos, size_t* b, size_t* e) {
+  size_t q = s.find('"', pos);
+  if (q == std::string::npos) return false;
+  size_t r = s.find('"', q + 1);
+  if (r == std::string::npos) return false;
+  *b = q + 1;
+  *e = r;
+  return true;
+}
+static bool hex_decode(const std::string& s, size_t b, size_t e, uint8_t* out, size_t want) {
+  if (e - b >= 2 && s[b] == '0' && s[b + 1] == 'x') b += 2;
+  if (e - b != 2 * want) return false;
+  auto nib = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  for (size_t i = 0; i < want; i++) {
+    int h = nib(s[b + 2 * i]), l = nib(s[b + 2 * i + 1]);
+    if (h < 0 || l < 0) return false;
+    out[i] = (uint8_t)(h * 16 + l);
+  }
+  return true;
+}
+static bool json_field(const std::string& s, const char* key, uint8_t* out, size_t want) {
+  std::string k = std::string("\"") + key + "\"";
+  size_t p = s.find(k);
+  if (p == std::string::npos) return false;
+  p = s.find(':', p + k.size());
+  if (p == std::string::npos) return false;
+  size_t b, e;
+  return json_str_after(s, p, &b, &e) && hex_decode(s, b, e, out, want);
+}
+
+extern "C" int zg_vk_load_json(zg_ctx* ctx, int kind, const char* json, size_t len) {
+  if (!ctx || !json) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  std::string s(json, len);
+  RawVK raw;
+  memset(&raw, 0, sizeof(raw));
+  if (!json_field(s, "alphaG1", raw.alpha_g1, 96) || !json_field(s, "betaG1", raw.beta_g1, 96) ||
+      !json_field(s, "betaG2", raw.beta_g2, 192) || !json_field(s, "gammaG2", raw.gamma_g2, 192) ||
+      !json_field(s, "deltaG1", raw.delta_g1, 96) || !json_field(s, "deltaG2", raw.delta_g2, 192))
+    return fail(ctx, ZG_E_VK, "Expected hex string of the right length");
+  size_t p = s.find("\"ic\"");
+  if (p == std::string::npos) return fail(ctx, ZG_E_VK, "missing ic");
+  p = s.find('[', p);
+  size_t end = s.find(']', p);
+  if (p == std::string::npos || end == std::string::npos) return fail(ctx, ZG_E_VK, "bad ic");
+  int n = 0;
+  size_t b, e;
+  while (json_str_after(s, p, &b, &e) && e < end) {
+    if (n >= ZG_MAX_IC) return fail(ctx, ZG_E_VK, "ic longer than 10");
+    if (!hex_decode(s, b, e, raw.ic[n], 96)) return fail(ctx, ZG_E_VK, "Expected hex string of length 96");
+    n++;
+    p = e + 1;
+  }
+  raw.n_ic = n;
+  return vk_upload(ctx, kind, raw);
+}
+
+extern "C" int zg_vk_load_builtin(zg_ctx* ctx, int kind) {
+  if (!ctx || kind < 0 || kind >= ZG_NKINDS) return ZG_E_INVAL;
+  const char* j = ZG_VK_JSON[kind];
+  return zg_vk_load_json(ctx, kind, j, strlen(j));
+}
+
+static int f12_download(zg_ctx* ctx, const Fq12* d, int count, uint8_t* out) {
+  hipLaunchKernelGGL(k_f12_to_bytes, dim3(nblocks(count)), dim3(ZG_BLOCK), 0, ctx->stream, d, count, ctx->d_bytes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, ctx->d_bytes, (size_t)576 * count, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+extern "C" int zg_vk_alpha_beta(zg_ctx* ctx, int kind, uint8_t gt[576]) {
+  if (!ctx || kind < 0 || kind >= ZG_NKINDS) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->vk_loaded[kind]) return fail(ctx, ZG_E_NOVK, "verifying key not loaded");
+  HIPCHK(hipSetDevice(ctx->device));
+  return f12_download(ctx, &ctx->d_vk[kind].alpha_beta, 1, gt);
+}
+
+// ------------------------------------------------------------------ single proof (parity path)
+extern "C" int zg_verify_one_gt(zg_ctx* ctx, int kind, const uint8_t proof[192], const uint8_t* inputs,
+                                size_t n_inputs, uint8_t* status, uint8_t gt[576]) {
+  if (!ctx || kind < 0 || kind >= ZG_NKINDS || !proof || !status || n_inputs > 255) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->vk_loaded[kind]) return fail(ctx, ZG_E_NOVK, "verifying key not loaded");
+  HIPCHK(hipSetDevice(ctx->device));
+  uint8_t in[288];
+  memset(in, 0, sizeof(in));
+  size_t kk = n_inputs < ZG_MAX_INPUTS ? n_inputs : ZG_MAX_INPUTS;
+  if (kk) memcpy(in, inputs, 32 * kk);
+  uint8_t k8 = (uint8_t)n_inputs, kind8 = (uint8_t)kind;
+  HIPCHK(hipMemcpyAsync(ctx->d_proofs, proof, 192, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_inputs, in, 288, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_kinds, &kind8, 1, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_ninputs, &k8, 1, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_verify_single, dim3(1), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_vk, 1, ctx->d_proofs,
+                     ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs, ctx->d_status, ctx->d_bytes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(status, ctx->d_status, 1, hipMemcpyDeviceToHost, ctx->stream));
+  if (gt) HIPCHK(hipMemcpyAsync(gt, ctx->d_bytes, 576, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+extern "C" int zg_verify_each(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
+                              const uint8_t* inputs, const uint8_t* n_inputs, uint8_t* status, uint8_t* gts) {
+  if (!ctx || (n && (!proofs || !kinds || !inputs || !status))) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
+  HIPCHK(hipSetDevice(ctx->device));
+  for (size_t i = 0; i < n; i++)
+    if (kinds[i] >= ZG_NKINDS || !ctx->vk_loaded[kinds[i]]) return fail(ctx, ZG_E_NOVK, "verifying key not loaded");
+  if (!n) return ZG_OK;
+  uint8_t* d_gts = nullptr;
+  if (gts) HIPCHK(hipMalloc(&d_gts, 576 * n));
+  HIPCHK(hipMemcpyAsync(ctx->d_proofs, proofs, 192 * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_kinds, kinds, n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->d_inputs, inputs, 288 * n, hipMemcpyHostToDevice, ctx->stream));
+  if (n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, n_inputs, n, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_verify_single, dim3(nblocks(n)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_vk, (int)n,
+                     ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, n_inputs ? ctx->d_ninputs : nullptr, ctx->d_status,
+                     d_gts);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(status, ctx->d_status, n, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && gts) e = hipMemcpyAsync(gts, d_gts, 576 * n, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (d_gts) hipFree(d_gts);
+  if (e != hipSuccess) return fail(ctx, ZG_E_HIP, std::string("zg_verify_each: ") + hipGetErrorString(e));
+  return ZG_OK;
+}
+
+// ------------------------------------------------------------------ batch
+static void gen_scalars(zg_ctx* ctx, size_t n, std::vector<uint8_t>& r) {
+  r.resize(n * 16);
+  if (ctx->seeded) {
+    for (size_t i = 0; i < n; i++) {
+      Blake2b h(16);
+      h.update("zg-batch-r", 10);
+      uint8_t le[8];
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)(ctx->seed >> (8 * b));
+      h.update(le, 8);
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)((uint64_t)i >> (8 * b));
+      h.update(le, 8);
+      h.final(&r[16 * i]);
+    }
+  } else {
+    size_t off = 0;
+    while (off < r.size()) {
+      ssize_t got = getrandom(&r[off], r.size() - off, 0);
+      if (got < 0) {
+        if (errno == EINTR) continue;
+        break;
+      }
+      off += (size_t)got;
+    }
+  }
+  for (size_t i = 0; i < n; i++) {  // r_i != 0
+    uint8_t acc = 0;
+    for (int b = 0; b < 16; b++) acc |= r[16 * i + b];
+    if (!acc) r[16 * i] = 1;
+  }
+}
+
+static BatchBufs batch_bufs(zg_ctx* ctx) {
+  BatchBufs b;
+  b.vks = ctx->d_vk;
+  b.proofs = ctx->d_proofs;
+  b.kinds = ctx->d_kinds;
+  b.inputs = ctx->d_inputs;
+  b.ninputs = ctx->cur_ninputs;
+  b.r = ctx->d_r;
+  b.status = ctx->d_status;
+  b.ptA = ctx->d_ptA;
+  b.ptB = ctx->d_ptB;
+  b.ftree = ctx->d_ftree;
+  b.ctree = ctx->d_ctree;
+  b.stree = ctx->d_stree;
+  b.n = (int)ctx->n;
+  b.npad = (int)ctx->npad;
+  return b;
+}
+
+// the pipeline on device-resident inputs already in ctx buffers
+static int run_pipeline(zg_ctx* ctx) {
+  BatchBufs b = batch_bufs(ctx);
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  hipLaunchKernelGGL(k_batch_decode, dim3(nblocks(ctx->npad)), dim3(ZG_BLOCK), 0, ctx->stream, b);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  hipLaunchKernelGGL(k_batch_miller, dim3(nblocks(ctx->npad)), dim3(ZG_BLOCK), 0, ctx->stream, b);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
+    hipLaunchKernelGGL(k_tree_level, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  return ZG_OK;
+}
+
+static int check_kinds(zg_ctx* ctx, size_t n, const uint8_t* kinds) {
+  for (size_t i = 0; i < n; i++) {
+    if (kinds[i] >= ZG_NKINDS) return fail(ctx, ZG_E_INVAL, "bad kind at " + std::to_string(i));
+    if (!ctx->vk_loaded[kinds[i]]) return fail(ctx, ZG_E_NOVK, "verifying key not loaded for proof " + std::to_string(i));
+  }
+  return ZG_OK;
+}
+
+static int begin_common(zg_ctx* ctx, size_t n) {
+  if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
+  ctx->n = n;
+  size_t npad = 1;
+  while (npad < n) npad <<= 1;
+  ctx->npad = npad;
+  ctx->calls++;
+  return ZG_OK;
+}
+
+extern "C" int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
+                              const uint8_t* inputs, const uint8_t* n_inputs, const uint8_t* r) {
+  if (!ctx || (n && (!proofs || !kinds || !inputs))) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = begin_common(ctx, n);
+  if (rc) return rc;
+  if ((rc = check_kinds(ctx, n, kinds))) return rc;
+  std::vector<uint8_t> rr;
+  if (!r) {
+    gen_scalars(ctx, n, rr);
+    r = rr.data();
+  }
+  if (n) {
+    HIPCHK(hipMemcpyAsync(ctx->d_proofs, proofs, n * 192, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_kinds, kinds, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_inputs, inputs, n * 288, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_r, r, n * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, n_inputs, n, hipMemcpyHostToDevice, ctx->stream));
+  }
+  ctx->cur_ninputs = n_inputs ? ctx->d_ninputs : nullptr;
+  if ((rc = run_pipeline(ctx))) return rc;
+  ctx->state = 1;
+  return ZG_OK;
+}
+
+extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,
+                                     const void* d_inputs, const void* d_n_inputs, const void* d_r) {
+  if (!ctx || (n && (!d_proofs || !d_kinds || !d_inputs))) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = begin_common(ctx, n);
+  if (rc) return rc;
+  for (int k = 0; k < ZG_NKINDS; k++)
+    if (!ctx->vk_loaded[k]) {
+      // device-resident kinds are not inspected on the host: require every VK loaded
+      return fail(ctx, ZG_E_NOVK, "device batches need all three verifying keys loaded");
+    }
+  if (n) {
+    HIPCHK(hipMemcpyAsync(ctx->d_proofs, d_proofs, n * 192, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_kinds, d_kinds, n, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_inputs, d_inputs, n * 288, hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_r) {
+      HIPCHK(hipMemcpyAsync(ctx->d_r, d_r, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+      std::vector<uint8_t> rr;
+      gen_scalars(ctx, n, rr);
+      HIPCHK(hipMemcpyAsync(ctx->d_r, rr.data(), n * 16, hipMemcpyHostToDevice, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    if (d_n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, d_n_inputs, n, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  ctx->cur_ninputs = d_n_inputs ? ctx->d_ninputs : nullptr;
+  if ((rc = run_pipeline(ctx))) return rc;
+  ctx->state = 1;
+  return ZG_OK;
+}
+
+// check a list of tree nodes; mode per k_node_final. ok / out are host arrays (may be null)
+static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std::vector<int>* ok, uint8_t* out_bytes) {
+  BatchBufs b = batch_bufs(ctx);
+  if (ok) ok->assign(nodes.size(), 0);
+  for (size_t off = 0; off < nodes.size(); off += ZG_NODE_CHUNK) {
+    int m = (int)std::min((size_t)ZG_NODE_CHUNK, nodes.size() - off);
+    HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
+    NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, m};
+    hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)m * ZG_NKINDS * ZG_MSM_SLOTS)), dim3(ZG_BLOCK), 0,
+                       ctx->stream, b, nb);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_node_pairs, dim3(nblocks((size_t)m * ZG_NKINDS * ZG_NPAIRS)), dim3(ZG_BLOCK), 0,
+                       ctx->stream, b, nb);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_node_final, dim3(nblocks(m)), dim3(ZG_BLOCK), 0, ctx->stream, b, nb, mode);
+    HIPCHK(hipGetLastError());
+    if (ok) HIPCHK(hipMemcpyAsync(ok->data() + off, ctx->d_ok, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (out_bytes) {
+      int rc = f12_download(ctx, ctx->d_out, m, out_bytes + (size_t)576 * off);
+      if (rc) return rc;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
+  if (!ctx || !partial) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_partial before zg_batch_begin");
+  HIPCHK(hipSetDevice(ctx->device));
+  std::vector<int> root = {1};
+  int rc = check_nodes(ctx, root, 1, nullptr, partial);
+  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  HIPCHK(hipEventSynchronize(ctx->ev[4]));
+  for (int i = 0; i < 4; i++) hipEventElapsedTime(&ctx->timings[i], ctx->ev[i], ctx->ev[i + 1]);
+  return rc;
+}
+
+extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok) {
+  if (!ctx || !partials || !ok || count == 0 || count > ZG_NODE_CHUNK) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(ctx->d_bytes, partials, 576 * count, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_f12_from_bytes, dim3(nblocks(count)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_bytes, (int)count,
+                     ctx->d_pairf);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(1), 0, ctx->stream, ctx->d_pairf, (int)count, ctx->d_ok,
+                     ctx->d_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ok, ctx->d_ok, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+// Bisection over the product trees: a failing node's children are re-checked exactly;
+// a failing leaf is a proof whose own check fails (r_i != 0 makes it bellman's check).
+static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
+  std::vector<int> level = {1};
+  const int npad = (int)ctx->npad, n = (int)ctx->n;
+  while (!level.empty()) {
+    std::vector<int> ok;
+    int rc = check_nodes(ctx, level, 0, &ok, nullptr);
+    if (rc) return rc;
+    std::vector<int> next;
+    for (size_t q = 0; q < level.size(); q++) {
+      if (ok[q]) continue;
+      int node = level[q];
+      if (node >= npad) {
+        int i = node - npad;
+        if (i < n && st[i] == ST_PENDING) st[i] = ST_VERIFY_FAILED;
+        continue;
+      }
+      // children that start at or beyond n hold only padding (identity): skip them
+      for (int c = 2 * node; c <= 2 * node + 1; c++) {
+        int depth_span = 1;
+        int x = c;
+        while (x < npad) {
+          x <<= 1;
+          depth_span <<= 1;
+        }
+        int first = x - npad;
+        if (first < n) next.push_back(c);
+      }
+    }
+    level.swap(next);
+  }
+  return ZG_OK;
+}
+
+extern "C" int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status) {
+  if (!ctx || !status) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_finish before zg_batch_begin");
+  HIPCHK(hipSetDevice(ctx->device));
+  std::vector<uint8_t> st(ctx->n);
+  if (ctx->n) HIPCHK(hipMemcpyAsync(st.data(), ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (!batch_ok) {
+    int rc = bisect(ctx, st);
+    if (rc) return rc;
+  }
+  for (size_t i = 0; i < ctx->n; i++) status[i] = st[i] == ST_PENDING ? ST_OK : st[i];
+  ctx->state = 0;
+  return ZG_OK;
+}
+
+extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
+                               const uint8_t* inputs, const uint8_t* n_inputs, const uint8_t* r, uint8_t* status,
+                               uint8_t* gt_out) {
+  if (!ctx || !status) return ZG_E_INVAL;
+  int rc = zg_batch_begin(ctx, n, proofs, kinds, inputs, n_inputs, r);
+  if (rc) return rc;
+  int ok = 1;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    std::vector<int> root = {1}, okv;
+    if (gt_out && (rc = check_nodes(ctx, root, 2, nullptr, gt_out))) return rc;
+    if ((rc = check_nodes(ctx, root, 0, &okv, nullptr))) return rc;
+    ok = okv[0];
+  }
+  return zg_batch_finish(ctx, ok, status);
+}
+
+extern "C" int zg_last_timings(zg_ctx* ctx, float* ms4) {
+  if (!ctx || !ms4) return ZG_E_INVAL;
+  for (int i = 0; i < 4; i++) ms4[i] = ctx->timings[i];
+  return ZG_OK;
+}
+
+// ------------------------------------------------------------------ synthetic workload
+static void reduce_mod_r(uint8_t* le32) {
+  // value < 2^256 < 3r: subtract r while >= r
+  for (int rep = 0; rep < 3; rep++) {
+    uint32_t v[8];
+    for (int w = 0; w < 8; w++)
+      v[w] = (uint32_t)le32[4 * w] | ((uint32_t)le32[4 * w + 1] << 8) | ((uint32_t)le32[4 * w + 2] << 16) |
+             ((uint32_t)le32[4 * w + 3] << 24);
+    uint32_t d[8], borrow = 0;
+    for (int w = 0; w < 8; w++) {
+      uint64_t t = (uint64_t)v[w] - FR_R[w] - borrow;
+      d[w] = (uint32_t)t;
+      borrow = (uint32_t)(t >> 63);
+    }
+    if (borrow) return;
+    for (int w = 0; w < 8; w++)
+      for (int b = 0; b < 4; b++) le32[4 * w + b] = (uint8_t)(d[w] >> (8 * b));
+  }
+}
+
+extern "C" int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, const uint8_t* src_kinds,
+                                    size_t n, const uint32_t* src_index, uint64_t seed, uint8_t* out_proofs) {
+  if (!ctx || !src_proofs || !src_kinds || !src_index || !out_proofs || n_src == 0) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  for (size_t i = 0; i < n_src; i++)
+    if (src_kinds[i] >= ZG_NKINDS || !ctx->vk_loaded[src_kinds[i]]) return fail(ctx, ZG_E_NOVK, "source kind VK");
+  for (size_t i = 0; i < n; i++)
+    if (src_index[i] >= n_src) return fail(ctx, ZG_E_INVAL, "src_index out of range");
+  std::vector<uint32_t> ts(16 * n);
+  for (size_t i = 0; i < n; i++) {
+    Blake2b h(64);
+    h.update("zg-rerand", 9);
+    uint8_t le[8];
+    for (int b = 0; b < 8; b++) le[b] = (uint8_t)(seed >> (8 * b));
+    h.update(le, 8);
+    for (int b = 0; b < 8; b++) le[b] = (uint8_t)((uint64_t)i >> (8 * b));
+    h.update(le, 8);
+    uint8_t dg[64];
+    h.final(dg);
+    for (int half = 0; half < 2; half++) {
+      uint8_t* x = dg + 32 * half;
+      reduce_mod_r(x);
+      uint8_t acc = 0;
+      for (int b = 0; b < 32; b++) acc |= x[b];
+      if (!acc) x[0] = 1;
+      for (int w = 0; w < 8; w++)
+        ts[16 * i + 8 * half + w] = (uint32_t)x[4 * w] | ((uint32_t)x[4 * w + 1] << 8) |
+                                    ((uint32_t)x[4 * w + 2] << 16) | ((uint32_t)x[4 * w + 3] << 24);
+    }
+  }
+  uint8_t *d_src, *d_sk, *d_out;
+  uint32_t *d_idx, *d_ts;
+  HIPCHK(hipMalloc(&d_src, 192 * n_src));
+  HIPCHK(hipMalloc(&d_sk, n_src));
+  HIPCHK(hipMalloc(&d_out, 192 * (n ? n : 1)));
+  HIPCHK(hipMalloc(&d_idx, 4 * (n ? n : 1)));
+  HIPCHK(hipMalloc(&d_ts, 64 * (n ? n : 1)));
+  int rc = ZG_OK;
+  if (hipMemcpy(d_src, src_proofs, 192 * n_src, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_sk, src_kinds, n_src, hipMemcpyHostToDevice) != hipSuccess ||
+      (n && hipMemcpy(d_idx, src_index, 4 * n, hipMemcpyHostToDevice) != hipSuccess) ||
+      (n && hipMemcpy(d_ts, ts.data(), 64 * n, hipMemcpyHostToDevice) != hipSuccess)) {
+    rc = fail(ctx, ZG_E_HIP, "copy");
+  } else if (n) {
+    hipLaunchKernelGGL(k_rerandomize, dim3(nblocks(n)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_vk, d_src, d_sk, d_idx,
+                       d_ts, (int)n, d_out);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess ||
+        hipMemcpy(out_proofs, d_out, 192 * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(ctx, ZG_E_HIP, "rerandomize kernel");
+  }
+  hipFree(d_src);
+  hipFree(d_sk);
+  hipFree(d_out);
+  hipFree(d_idx);
+  hipFree(d_ts);
+  return rc;
+}
+
+extern "C" int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s) {
+  if (!ctx || !macs_per_s) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  const int blocks = 256 * 16, threads = 256, iters = 2048;
+  hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, 16, 1u);
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, iters, 1u);
+  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  HIPCHK(hipEventSynchronize(ctx->ev[1]));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+  *macs_per_s = (double)blocks * threads * iters * 64.0 / (ms * 1e-3);
+  return ZG_OK;
+}

@@ -1,0 +1,299 @@
+// zg_kernels.h -- the gfx950 kernels of the batch verifier.
+//
+// Batch algebra: with 128-bit random r_i a batch of proofs is valid iff
+//   FE( prod_i ML(r_i A_i, B_i)
+//       * prod_k ML(sum_{i in k} r_i acc_i, -gamma_k) * ML(sum_{i in k} r_i C_i, -delta_k)
+//       * ML(-(sum_{i in k} r_i) alpha_k, beta_k) ) == 1
+// and sum_i r_i acc_i = S_k0 ic_k[0] + sum_j S_kj ic_k[j] with S_k0 = sum r_i,
+// S_kj = sum r_i x_ij (Fr). Per-proof values are kept in complete binary product trees
+// (heap layout, leaves at npad + i) so any contiguous node can be re-checked exactly:
+// bisection on failure re-uses them.
+#pragma once
+#include "zg_groth16.h"
+
+namespace zg {
+
+#define ZG_MSM_SLOTS (ZG_MAX_IC + 1)  // ic terms + the alpha term
+#define ZG_NPAIRS 3                   // per kind: (acc,-gamma) (C,-delta) (-S alpha, beta)
+
+__device__ __constant__ const int KIND_NINPUTS[ZG_NKINDS] = {7, 5, 9};
+
+struct BatchBufs {
+  const DevVK* vks;
+  const uint8_t* proofs;   // n x 192
+  const uint8_t* kinds;    // n
+  const uint8_t* inputs;   // n x 288
+  const uint8_t* ninputs;  // n or null
+  const uint8_t* r;        // n x 16
+  uint8_t* status;         // n
+  G1A* ptA;                // npad: r_i A_i (affine)
+  G2A* ptB;                // npad: B_i
+  Fq12* ftree;             // 2 npad
+  G1J* ctree;              // 2 npad x 3 kinds
+  Fr* stree;               // 2 npad x 3 kinds x ZG_MAX_IC (Montgomery)
+  int n, npad;
+};
+
+// K1 + K2 + K3: decode/subgroup-check A, B, C; public-input canonicity and count; r_i A_i;
+// r_i C_i and the Fr scalars r_i, r_i x_ij as tree leaves.
+__global__ void __launch_bounds__(64) k_batch_decode(BatchBufs b) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.npad) return;
+  const int leaf = b.npad + i;
+  for (int k = 0; k < ZG_NKINDS; k++) {
+    b.ctree[leaf * ZG_NKINDS + k] = jac_infinity<Fq>();
+    for (int m = 0; m < ZG_MAX_IC; m++) b.stree[(leaf * ZG_NKINDS + k) * ZG_MAX_IC + m] = fp_zero<FrM>();
+  }
+  b.ptA[i].inf = true;
+  if (i >= b.n) return;
+  const int kind = b.kinds[i];
+  const DevVK& vk = b.vks[kind];
+  const int k = b.ninputs ? b.ninputs[i] : KIND_NINPUTS[kind];
+  const int kk = k < ZG_MAX_INPUTS ? k : ZG_MAX_INPUTS;
+  Fr x[ZG_MAX_INPUTS];
+  uint8_t st = ST_PENDING;
+  G1A a, c;
+  G2A bb;
+  if (!inputs_canonical(b.inputs + (size_t)i * 288, kk, x))
+    st = ST_INPUT_NONCANONICAL;
+  else if (!proof_decode(b.proofs + (size_t)i * 192, &a, &bb, &c))
+    st = ST_DECODE_INVALID;
+  else if (k + 1 != vk.ic_len)
+    st = ST_MALFORMED_VK;
+  b.status[i] = st;
+  if (st != ST_PENDING) return;
+  uint32_t rl[4];
+  const uint8_t* rp = b.r + (size_t)i * 16;
+  for (int w = 0; w < 4; w++)
+    rl[w] = (uint32_t)rp[4 * w] | ((uint32_t)rp[4 * w + 1] << 8) | ((uint32_t)rp[4 * w + 2] << 16) |
+            ((uint32_t)rp[4 * w + 3] << 24);
+  b.ptA[i] = jac_to_aff(jac_mul_limbs(a, rl, 128));
+  b.ptB[i] = bb;
+  b.ctree[leaf * ZG_NKINDS + kind] = jac_mul_limbs(c, rl, 128);
+  Fr rf = fp_zero<FrM>();
+  for (int w = 0; w < 4; w++) rf.l[w] = rl[w];
+  rf = fr_to_mont(rf);
+  Fr* s = b.stree + (leaf * ZG_NKINDS + kind) * ZG_MAX_IC;
+  s[0] = rf;
+  for (int j = 0; j < kk; j++) s[1 + j] = fr_mul(rf, fr_to_mont(x[j]));
+}
+
+// K6 (per proof): f_i = ML(r_i A_i, B_i) -> ftree leaf
+__global__ void __launch_bounds__(64) k_batch_miller(BatchBufs b) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.npad) return;
+  Fq12 f = f12_one();
+  if (i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf) f = miller_loop_1(b.ptA[i], b.ptB[i]);
+  b.ftree[b.npad + i] = f;
+}
+
+// product-tree level: nodes [lo, 2 lo)
+__global__ void __launch_bounds__(64) k_tree_level(BatchBufs b, int lo) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= lo) return;
+  const int node = lo + j, l = 2 * node, r = 2 * node + 1;
+  b.ftree[node] = f12_mul(b.ftree[l], b.ftree[r]);
+  for (int k = 0; k < ZG_NKINDS; k++) {
+    b.ctree[node * ZG_NKINDS + k] = jac_add(b.ctree[l * ZG_NKINDS + k], b.ctree[r * ZG_NKINDS + k]);
+    for (int m = 0; m < ZG_MAX_IC; m++)
+      b.stree[(node * ZG_NKINDS + k) * ZG_MAX_IC + m] =
+          fr_add(b.stree[(l * ZG_NKINDS + k) * ZG_MAX_IC + m], b.stree[(r * ZG_NKINDS + k) * ZG_MAX_IC + m]);
+  }
+}
+
+struct NodeBufs {
+  const int* nodes;  // M tree node ids
+  G1J* msm;          // M x 3 x ZG_MSM_SLOTS
+  Fq12* pairf;       // M x 3 x ZG_NPAIRS
+  int* ok;           // M
+  Fq12* out;         // M
+  int m;
+};
+
+// VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k
+__global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb.m * ZG_NKINDS * ZG_MSM_SLOTS) return;
+  const int idx = t / (ZG_NKINDS * ZG_MSM_SLOTS);
+  const int kind = (t / ZG_MSM_SLOTS) % ZG_NKINDS;
+  const int j = t % ZG_MSM_SLOTS;
+  const int node = nb.nodes[idx];
+  const DevVK& vk = b.vks[kind];
+  G1J res = jac_infinity<Fq>();
+  if (vk.loaded) {
+    const Fr* s = b.stree + (node * ZG_NKINDS + kind) * ZG_MAX_IC;
+    if (j < vk.ic_len) {
+      Fr sc = fr_from_mont(s[j]);
+      res = jac_mul_limbs(vk.ic[j], sc.l, 255);
+    } else if (j == ZG_MAX_IC && !vk.alpha.inf) {
+      Fr sc = fr_from_mont(fp_neg<FrM>(s[0]));
+      res = jac_mul_limbs(vk.alpha, sc.l, 255);
+    }
+  }
+  nb.msm[t] = res;
+}
+
+// VK-side Miller loops per checked node, with the prepared lines of the VK
+__global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb.m * ZG_NKINDS * ZG_NPAIRS) return;
+  const int idx = t / (ZG_NKINDS * ZG_NPAIRS);
+  const int kind = (t / ZG_NPAIRS) % ZG_NKINDS;
+  const int pair = t % ZG_NPAIRS;
+  const int node = nb.nodes[idx];
+  const DevVK& vk = b.vks[kind];
+  Fq12 f = f12_one();
+  if (vk.loaded) {
+    const G1J* ms = nb.msm + (idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS;
+    G1J pj = jac_infinity<Fq>();
+    const Line* lines = nullptr;
+    if (pair == 0 && !vk.gamma.inf) {
+      for (int j = 0; j < vk.ic_len; j++) pj = jac_add(pj, ms[j]);
+      lines = vk.neg_gamma_lines;
+    } else if (pair == 1 && !vk.delta.inf) {
+      pj = b.ctree[node * ZG_NKINDS + kind];
+      lines = vk.neg_delta_lines;
+    } else if (pair == 2 && !vk.beta.inf) {
+      pj = ms[ZG_MAX_IC];
+      lines = vk.beta_lines;
+    }
+    if (lines) {
+      G1A p = jac_to_aff(pj);
+      if (!p.inf) f = miller_loop_prepared(p, lines);
+    }
+  }
+  nb.pairf[t] = f;
+}
+
+// mode 0: FE(product) == 1 -> ok ; mode 1: write product (Miller partial) ;
+// mode 2: FE(product without the alpha/beta pairs) -> out (accumulated GT)
+__global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int mode) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nb.m) return;
+  Fq12 f = b.ftree[nb.nodes[idx]];
+  for (int k = 0; k < ZG_NKINDS; k++)
+    for (int p = 0; p < ZG_NPAIRS; p++) {
+      if (mode == 2 && p == 2) continue;
+      f = f12_mul(f, nb.pairf[(idx * ZG_NKINDS + k) * ZG_NPAIRS + p]);
+    }
+  if (mode == 1) {
+    nb.out[idx] = f;
+    return;
+  }
+  Fq12 g = final_exponentiation(f);
+  if (mode == 2) nb.out[idx] = g;
+  nb.ok[idx] = f12_is_one(g) ? 1 : 0;
+}
+
+// K7 across ranks: product of partials, one final exponentiation, == 1 ?
+__global__ void k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
+  if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
+  Fq12 f = f12_one();
+  for (int c = 0; c < count; c++) f = f12_mul(f, parts[c]);
+  Fq12 g = final_exponentiation(f);
+  *gt = g;
+  *ok = f12_is_one(g) ? 1 : 0;
+}
+
+__global__ void k_f12_to_bytes(const Fq12* a, int count, uint8_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) f12_to_bytes(a[i], out + (size_t)576 * i);
+}
+__global__ void k_f12_from_bytes(const uint8_t* in, int count, Fq12* a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) a[i] = f12_from_bytes(in + (size_t)576 * i);
+}
+
+// prepare_verifying_key (one thread)
+__global__ void k_vk_prepare(const RawVK* raw, DevVK* vk, int* err) {
+  if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
+  *err = vk_prepare(*raw, vk);
+}
+
+// bellman-exact single-proof verification (K-per-proof; parity path and leaf checks)
+__global__ void __launch_bounds__(64) k_verify_single(const DevVK* vks, int n, const uint8_t* proofs,
+                                                       const uint8_t* kinds, const uint8_t* inputs,
+                                                       const uint8_t* ninputs, uint8_t* status, uint8_t* gts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int kind = kinds[i];
+  const int k = ninputs ? ninputs[i] : KIND_NINPUTS[kind];
+  Fq12 gt;
+  uint8_t st;
+  if (k > ZG_MAX_INPUTS) {
+    Fr x[ZG_MAX_INPUTS];
+    G1A a, c;
+    G2A bb;
+    if (!inputs_canonical(inputs + (size_t)i * 288, ZG_MAX_INPUTS, x))
+      st = ST_INPUT_NONCANONICAL;
+    else if (!proof_decode(proofs + (size_t)i * 192, &a, &bb, &c))
+      st = ST_DECODE_INVALID;
+    else
+      st = ST_MALFORMED_VK;
+  } else {
+    st = verify_single(vks[kind], proofs + (size_t)i * 192, inputs + (size_t)i * 288, k, &gt);
+  }
+  status[i] = st;
+  if (gts && (st == ST_OK || st == ST_VERIFY_FAILED)) f12_to_bytes(gt, gts + (size_t)576 * i);
+}
+
+ZG_INL Fr fr_pow_limbs(const Fr& a, const uint32_t* e, int nbits) {
+  Fr r = fr_one();
+  for (int i = nbits - 1; i >= 0; i--) {
+    r = fr_mul(r, r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fr_mul(r, a);
+  }
+  return r;
+}
+
+// synthetic workload: Groth16 re-randomization (A,B,C) -> (t^-1 A, t(B + s delta), C + s A)
+__global__ void __launch_bounds__(64) k_rerandomize(const DevVK* vks, const uint8_t* src, const uint8_t* src_kinds,
+                                                     const uint32_t* src_index, const uint32_t* ts, int n,
+                                                     uint8_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s_i = src_index[i];
+  G1A a, c;
+  G2A bb;
+  uint8_t* o = out + (size_t)192 * i;
+  if (!proof_decode(src + (size_t)192 * s_i, &a, &bb, &c)) {
+    for (int k = 0; k < 192; k++) o[k] = 0;
+    return;
+  }
+  const DevVK& vk = vks[src_kinds[s_i]];
+  Fr t, s;
+  for (int w = 0; w < 8; w++) {
+    t.l[w] = ts[16 * i + w];
+    s.l[w] = ts[16 * i + 8 + w];
+  }
+  Fr tinv = fr_from_mont(fr_pow_limbs(fr_to_mont(t), FR_EXP_INV, 255));
+  G1A a2 = jac_to_aff(jac_mul_limbs(a, tinv.l, 255));
+  G2J bs = jac_add(jac_from_aff(bb), jac_mul_limbs(vk.delta, s.l, 255));
+  G2A b2 = jac_to_aff(jac_mul_limbs(jac_to_aff(bs), t.l, 255));
+  G1A c2 = jac_to_aff(jac_add(jac_from_aff(c), jac_mul_limbs(a, s.l, 255)));
+  g1_compress(a2, o);
+  g2_compress(b2, o + 48);
+  g1_compress(c2, o + 144);
+}
+
+// v_mad_u64_u32 throughput probe: 8 independent 64-bit accumulator chains per lane,
+// 64 MACs per chain per iteration
+__global__ void __launch_bounds__(256) k_mad_rate(uint64_t* sink, int iters, uint32_t seed) {
+  uint32_t a = seed + threadIdx.x, b = seed * 3 + blockIdx.x;
+  uint64_t c[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) c[q] = a + q * b;
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) c[q] = (uint64_t)(uint32_t)c[q] * ((q & 1) ? a : b) + c[q];
+    }
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) x ^= c[q];
+  if (x == 0x123456789ull) sink[0] = x;
+}
+
+}  // namespace zg

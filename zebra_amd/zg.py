@@ -1,0 +1,189 @@
+"""ctypes binding of the C ABI (include/zg.h) -- the same calls a Rust `verification/gpu`
+module makes over `extern "C"`. Loads the in-tree zebra_amd/libzg.so and
+fails loudly if it is missing: there is no CPU fallback in the product path.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzg.so")
+
+KIND_SPEND, KIND_OUTPUT, KIND_SPROUT = 0, 1, 2
+KIND_NINPUTS = {KIND_SPEND: 7, KIND_OUTPUT: 5, KIND_SPROUT: 9}
+STATUS_OK, STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL = 0, 1, 2, 3, 4
+STATUS_NAMES = {0: "OK", 1: "DECODE_INVALID", 2: "MALFORMED_VK", 3: "VERIFY_FAILED", 4: "INPUT_NONCANONICAL"}
+PROOF_BYTES, INPUT_STRIDE, GT_BYTES, R_BYTES = 192, 288, 576, 16
+
+_lib = None
+
+
+class ZgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("zg error %d: %s" % (code, msg))
+        self.code = code
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("max_batch", ctypes.c_uint32), ("seeded", ctypes.c_int),
+                ("seed", ctypes.c_uint64)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("zebra_amd/libzg.so is not built (run __graft_entry__.build()); "
+                              "the GPU path has no fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u8p, sz, i = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int
+        L.zg_create.restype = vp
+        L.zg_create.argtypes = [ctypes.POINTER(_Config)]
+        L.zg_destroy.argtypes = [vp]
+        L.zg_last_error.restype = ctypes.c_char_p
+        L.zg_last_error.argtypes = [vp]
+        L.zg_version.restype = ctypes.c_char_p
+        L.zg_vk_load_builtin.argtypes = [vp, i]
+        L.zg_vk_load_json.argtypes = [vp, i, u8p, sz]
+        L.zg_vk_load_uncompressed.argtypes = [vp, i, u8p, u8p, u8p, u8p, u8p, u8p, sz, u8p]
+        L.zg_vk_alpha_beta.argtypes = [vp, i, u8p]
+        L.zg_verify_one_gt.argtypes = [vp, i, u8p, u8p, sz, u8p, u8p]
+        L.zg_verify_each.argtypes = [vp, sz, u8p, u8p, u8p, u8p, u8p, u8p]
+        L.zg_verify_batch.argtypes = [vp, sz, u8p, u8p, u8p, u8p, u8p, u8p, u8p]
+        L.zg_batch_begin.argtypes = [vp, sz, u8p, u8p, u8p, u8p, u8p]
+        L.zg_batch_begin_device.argtypes = [vp, sz, vp, vp, vp, vp, vp]
+        L.zg_batch_partial.argtypes = [vp, u8p]
+        L.zg_gt_check.argtypes = [vp, sz, u8p, ctypes.POINTER(i)]
+        L.zg_batch_finish.argtypes = [vp, i, u8p]
+        L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
+        L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def pack_inputs(rows):
+    """list (per proof) of lists of ints / 32-byte LE values -> n x 288 bytes"""
+    out = bytearray(INPUT_STRIDE * len(rows))
+    for i, row in enumerate(rows):
+        for j, x in enumerate(row):
+            b = x if isinstance(x, (bytes, bytearray)) else int(x).to_bytes(32, "little")
+            out[INPUT_STRIDE * i + 32 * j:INPUT_STRIDE * i + 32 * j + 32] = b
+    return bytes(out)
+
+
+class Context:
+    """One zg_ctx: a HIP stream, device buffers and the prepared VKs of one GPU."""
+
+    def __init__(self, device=0, max_batch=65536, seed=None, load_builtin=True):
+        L = lib()
+        cfg = _Config(device, max_batch, 1 if seed is not None else 0, seed or 0)
+        self._p = L.zg_create(ctypes.byref(cfg))
+        if not self._p:
+            raise ZgError(-2, "zg_create failed (no GPU / HIP error)")
+        if load_builtin:
+            for k in (KIND_SPEND, KIND_OUTPUT, KIND_SPROUT):
+                self.vk_load_builtin(k)
+
+    def close(self):
+        if self._p:
+            lib().zg_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise ZgError(rc, lib().zg_last_error(self._p).decode())
+
+    def vk_load_builtin(self, kind):
+        self._chk(lib().zg_vk_load_builtin(self._p, kind))
+
+    def vk_load_json(self, kind, text):
+        b = text.encode() if isinstance(text, str) else text
+        self._chk(lib().zg_vk_load_json(self._p, kind, b, len(b)))
+
+    def vk_load_uncompressed(self, kind, alpha_g1, beta_g1, beta_g2, gamma_g2, delta_g1, delta_g2, ic):
+        self._chk(lib().zg_vk_load_uncompressed(self._p, kind, alpha_g1, beta_g1, beta_g2, gamma_g2, delta_g1,
+                                                delta_g2, len(ic), b"".join(ic) if ic else None))
+
+    def alpha_beta(self, kind):
+        out = ctypes.create_string_buffer(GT_BYTES)
+        self._chk(lib().zg_vk_alpha_beta(self._p, kind, out))
+        return out.raw
+
+    def verify_one_gt(self, kind, proof, inputs):
+        """bellman verify_proof for one proof -> (status, GT bytes | None)."""
+        inp = pack_inputs([inputs])[:32 * len(inputs)] if inputs else b""
+        st = ctypes.create_string_buffer(1)
+        gt = ctypes.create_string_buffer(GT_BYTES)
+        self._chk(lib().zg_verify_one_gt(self._p, kind, bytes(proof), inp or None, len(inputs), st, gt))
+        s = st.raw[0]
+        return s, (gt.raw if s in (STATUS_OK, STATUS_VERIFY_FAILED) else None)
+
+    def verify_each(self, proofs, kinds, inputs, n_inputs=None, want_gt=True):
+        """per-proof bellman-exact verification -> (statuses, list of GT bytes | None)"""
+        n = len(kinds)
+        st = ctypes.create_string_buffer(max(n, 1))
+        gts = ctypes.create_string_buffer(max(GT_BYTES * n, 1)) if want_gt else None
+        self._chk(lib().zg_verify_each(self._p, n, bytes(proofs), bytes(kinds), bytes(inputs),
+                                       bytes(n_inputs) if n_inputs is not None else None, st, gts))
+        sts = list(st.raw[:n])
+        if not want_gt:
+            return sts, None
+        return sts, [gts.raw[GT_BYTES * i:GT_BYTES * (i + 1)] if sts[i] in (0, 3) else None for i in range(n)]
+
+    def verify_batch(self, proofs, kinds, inputs, n_inputs=None, r=None, want_gt=False):
+        """-> (list of statuses, accumulated GT bytes | None)"""
+        n = len(kinds)
+        st = ctypes.create_string_buffer(max(n, 1))
+        gt = ctypes.create_string_buffer(GT_BYTES) if want_gt else None
+        self._chk(lib().zg_verify_batch(self._p, n, bytes(proofs), bytes(kinds), bytes(inputs),
+                                        bytes(n_inputs) if n_inputs is not None else None,
+                                        bytes(r) if r is not None else None, st, gt))
+        return list(st.raw[:n]), (gt.raw if want_gt else None)
+
+    def batch_begin(self, proofs, kinds, inputs, n_inputs=None, r=None):
+        self._chk(lib().zg_batch_begin(self._p, len(kinds), bytes(proofs), bytes(kinds), bytes(inputs),
+                                       bytes(n_inputs) if n_inputs is not None else None,
+                                       bytes(r) if r is not None else None))
+
+    def batch_begin_device(self, n, d_proofs, d_kinds, d_inputs, d_n_inputs=None, d_r=None):
+        """device pointers (ints, e.g. torch tensor data_ptr()) of HBM-resident inputs"""
+        self._chk(lib().zg_batch_begin_device(self._p, n, d_proofs, d_kinds, d_inputs, d_n_inputs, d_r))
+
+    def batch_partial(self):
+        out = ctypes.create_string_buffer(GT_BYTES)
+        self._chk(lib().zg_batch_partial(self._p, out))
+        return out.raw
+
+    def gt_check(self, partials):
+        ok = ctypes.c_int(0)
+        self._chk(lib().zg_gt_check(self._p, len(partials), b"".join(partials), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def batch_finish(self, batch_ok, n):
+        st = ctypes.create_string_buffer(max(n, 1))
+        self._chk(lib().zg_batch_finish(self._p, 1 if batch_ok else 0, st))
+        return list(st.raw[:n])
+
+    def last_timings(self):
+        a = (ctypes.c_float * 4)()
+        self._chk(lib().zg_last_timings(self._p, a))
+        return list(a)
+
+    def synth_rerandomize(self, src_proofs, src_kinds, src_index, seed):
+        n = len(src_index)
+        idx = (ctypes.c_uint32 * max(n, 1))(*src_index)
+        out = ctypes.create_string_buffer(max(192 * n, 1))
+        self._chk(lib().zg_synth_rerandomize(self._p, len(src_kinds), bytes(src_proofs), bytes(src_kinds), n, idx,
+                                             seed, out))
+        return out.raw[:192 * n]
+
+    def bench_mad_rate(self):
+        v = ctypes.c_double(0)
+        self._chk(lib().zg_bench_mad_rate(self._p, ctypes.byref(v)))
+        return v.value
