@@ -97,6 +97,7 @@ def main():
     torch.cuda.set_device(local)
 
     from zebra_amd import Context
+    from zebra_amd.dist import combine_partials
     src_proofs, src_kinds, idx, kinds, inputs, shard = workload(rank, world, args.n)
     ctx = Context(device=local, max_batch=shard)
     t0 = time.perf_counter()
@@ -108,22 +109,14 @@ def main():
     d_proofs = torch.frombuffer(bytearray(proofs), dtype=torch.uint8).to(dev)
     d_kinds = torch.frombuffer(bytearray(kinds), dtype=torch.uint8).to(dev)
     d_inputs = torch.frombuffer(bytearray(inputs), dtype=torch.uint8).to(dev)
-    gathered = torch.zeros(world * 576, dtype=torch.uint8, device=dev)
-    okt = torch.zeros(1, dtype=torch.int32, device=dev)
     timings = []
 
     def step():
         ctx.batch_begin_device(shard, d_proofs.data_ptr(), d_kinds.data_ptr(), d_inputs.data_ptr())
         part = ctx.batch_partial()
         timings.append(ctx.last_timings())
-        if world > 1:
-            mine = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)
-            dist.all_gather_into_tensor(gathered, mine)          # RCCL over xGMI: 576 B per GPU
-            if rank == 0:
-                g = gathered.cpu().numpy().tobytes()
-                okt.fill_(1 if ctx.gt_check([g[576 * r:576 * r + 576] for r in range(world)]) else 0)
-            dist.broadcast(okt, 0)
-            ok = bool(okt.item())
+        if world > 1:   # RCCL over xGMI: 576 B per GPU, ONE final exponentiation on rank 0
+            ok = combine_partials(part, ctx.gt_check, world, rank, dev)
         else:
             ok = ctx.gt_check([part])
         return ok, ctx.batch_finish(ok, shard)

@@ -172,3 +172,36 @@ def batch_gt(lhs_list, r_list):
     for gt, r in zip(lhs_list, r_list):
         acc = B.f12_mul(acc, B.f12_pow(gt, r))
     return acc
+
+
+def batch_partial(pvks, items):
+    """The Miller partial F of a shard, exactly as the GPU forms it (not final-exponentiated):
+    prod_i ML(r_i A_i, B_i) * prod_k ML(acc_k, -gamma_k) ML(Csum_k, -delta_k) ML(-S_k alpha_k, beta_k)
+    over proofs that decode with a well-formed VK. items: (kind, proof bytes, inputs, r)."""
+    f = B.F12_ONE
+    sums = {k: [0] * len(p.ic) for k, p in pvks.items()}
+    csum = {k: None for k in pvks}
+    for kind, pb, inputs, r in items:
+        st, _ = (INPUT_NONCANONICAL, None) if any(x >= B.R for x in inputs) else (OK, None)
+        if st != OK:
+            continue
+        try:
+            a, b, c = proof_read(pb)
+        except B.DecodeError:
+            continue
+        pvk = pvks[kind]
+        if len(inputs) + 1 != len(pvk.ic):
+            continue
+        f = B.f12_mul(f, B.miller_loop([(B.ec_mul(B.FQ, a, r), B.g2_prepare(b))]))
+        sums[kind][0] = (sums[kind][0] + r) % B.R
+        for j, x in enumerate(inputs):
+            sums[kind][j + 1] = (sums[kind][j + 1] + r * x) % B.R
+        csum[kind] = B.ec_add(B.FQ, csum[kind], B.ec_mul(B.FQ, c, r))
+    for kind, pvk in pvks.items():
+        acc = None
+        for s, base in zip(sums[kind], pvk.ic):
+            acc = B.ec_add(B.FQ, acc, B.ec_mul(B.FQ, base, s))
+        nsa = B.ec_mul(B.FQ, pvk.vk.alpha_g1, (-sums[kind][0]) % B.R)
+        f = B.f12_mul(f, B.miller_loop([(acc, pvk.neg_gamma_g2), (csum[kind], pvk.neg_delta_g2),
+                                         (nsa, B.g2_prepare(pvk.vk.beta_g2))]))
+    return f

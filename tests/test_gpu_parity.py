@@ -159,3 +159,24 @@ def test_batch_4096_one_percent_corrupted(ctx):
             want[i] = 1
     sts, _ = ctx.verify_batch(bytes(proofs), bytes(src_kinds[j] for j in idx), pack_inputs(rows))
     assert sts == want
+
+
+def test_partial_bitexact_vs_oracle(ctx):
+    """the 576-byte Miller partial a rank contributes equals the oracle's batch_partial."""
+    import os
+    from oracle import bls12_381 as B, groth16 as G
+    from tests.conftest import ROOT
+    files = {0: "sapling-spend-verifying-key.json", 1: "sapling-output-verifying-key.json",
+             2: "sprout-groth16-key.json"}
+    pvks = {k: G.prepare_verifying_key(G.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", f)).read()))
+            for k, f in files.items()}
+    items = load_golden("batch64.json")["items"][:6]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    r = b"".join(bytes.fromhex(e["r"]) for e in items)
+    ctx.batch_begin(proofs, kinds, inputs, nin, r=r)
+    part = ctx.batch_partial()
+    ctx.batch_finish(True, len(items))
+    want = G.batch_partial(pvks, [(e["kind"], bytes.fromhex(e["proof"]),
+                                   [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]],
+                                   int.from_bytes(bytes.fromhex(e["r"]), "little")) for e in items])
+    assert part == B.f12_to_bytes(want)

@@ -1,0 +1,96 @@
+"""CPU tier: the N>1 protocol of zebra_amd.dist (all-gather of 576-byte Miller partials,
+ONE final exponentiation on rank 0, verdict broadcast) with world_size 2 over gloo.
+Partials are formed by the oracle (oracle.groth16.batch_partial, the same product the GPU
+forms per shard); the check is the oracle's final exponentiation of their product."""
+import os
+import socket
+
+import pytest
+
+from tests.conftest import ROOT, load_golden
+
+VK_FILES = {0: "sapling-spend-verifying-key.json", 1: "sapling-output-verifying-key.json",
+            2: "sprout-groth16-key.json"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _items(entries):
+    out = []
+    for e in entries:
+        out.append((e["kind"], bytes.fromhex(e["proof"]),
+                    [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]],
+                    int.from_bytes(bytes.fromhex(e["r"]), "little")))
+    return out
+
+
+def _worker(rank, world, port, shards, want, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from oracle import bls12_381 as B, groth16 as G
+    from zebra_amd.dist import combine_partials, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pvks = {k: G.prepare_verifying_key(G.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", f)).read()))
+                for k, f in VK_FILES.items()}
+        lo, hi = shard_range(len(shards), world, rank)
+        assert (lo, hi) == (rank, rank + 1)
+        part = B.f12_to_bytes(G.batch_partial(pvks, shards[rank]))
+
+        def check(parts):
+            f = B.F12_ONE
+            for p in parts:
+                f = B.f12_mul(f, B.f12_from_bytes(p))
+            return B.final_exponentiation(f) == B.F12_ONE
+
+        ok = combine_partials(part, check, world, rank, "cpu")
+        # a rank whose own partial fails its own check holds the failing shard
+        own = check([part])
+        q.put((rank, ok, own))
+        assert ok == want
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(shards, want):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, shards, want, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+@pytest.fixture(scope="module")
+def batch():
+    return load_golden("batch64.json")["items"]
+
+
+def test_two_ranks_all_valid(batch):
+    good = [e for e in batch if e["status"] == 0]
+    res = _run([_items(good[0:2]), _items(good[2:4])], True)
+    assert [r[1] for r in res] == [True, True]
+    assert [r[2] for r in res] == [True, True]
+
+
+def test_two_ranks_one_bad_shard(batch):
+    good = [e for e in batch if e["status"] == 0]
+    bad = [e for e in batch if e["status"] == 3]
+    res = _run([_items(good[0:2]), _items([bad[0], good[2]])], False)
+    assert [r[1] for r in res] == [False, False]       # verdict broadcast to both ranks
+    assert [r[2] for r in res] == [True, False]        # rank 1's own partial localises the failure
