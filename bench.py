@@ -144,8 +144,8 @@ def main():
 
     total = shard * world
     value = total * args.steps / dt
-    names = ["k_batch_decode", "k_batch_miller", "k_tree_level", "root_check"]
-    avg = [sum(t[i] for t in timings) / len(timings) for i in range(4)]
+    names = ["k_batch_decode", "k_batch_miller", "k_tree_f", "root_partial", "side_stream_vk", "device_pipeline"]
+    avg = [sum(t[i] for t in timings) / len(timings) for i in range(6)]
     dom = max(range(3), key=lambda i: avg[i])
     wk = {0: W_DECODE, 1: W_MILLER, 2: W_TREE}[dom]
     achieved = wk * MACS_PER_FQMUL * shard / (avg[dom] * 1e-3)

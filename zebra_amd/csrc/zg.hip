@@ -20,6 +20,7 @@ using namespace zg;
 
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
+#define ZG_NEV 8
 
 struct zg_ctx {
   int device = 0;
@@ -52,8 +53,10 @@ struct zg_ctx {
   int state = 0;
   size_t n = 0, npad = 0;
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
-  hipEvent_t ev[5] = {};
-  float timings[4] = {0, 0, 0, 0};
+  hipStream_t side = nullptr;  // VK-side root work, concurrent with the Miller kernel
+  int root_pairs_ready = 0;     // the pipeline already ran the root's MSM + VK pairs on `side`
+  hipEvent_t ev[ZG_NEV] = {};
+  float timings[6] = {0, 0, 0, 0, 0, 0};
   uint64_t calls = 0;
 };
 
@@ -89,7 +92,9 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ctx->cap = cap;
   ctx->seeded = cfg->seeded;
   ctx->seed = cfg->seed;
-  bool ok = hipSetDevice(ctx->device) == hipSuccess && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipSetDevice(ctx->device) == hipSuccess &&
+            hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) == hipSuccess;
   ok = ok && dalloc(&ctx->d_vk, ZG_NKINDS) == hipSuccess && dalloc(&ctx->d_rawvk, 1) == hipSuccess &&
        dalloc(&ctx->d_int, 16) == hipSuccess;
   ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
@@ -101,10 +106,10 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
        dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
        dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC) == hipSuccess;
   ok = ok && dalloc(&ctx->d_nodes, ZG_NODE_CHUNK) == hipSuccess &&
-       dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS) == hipSuccess &&
+       dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS) == hipSuccess &&
        dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS) == hipSuccess &&
        dalloc(&ctx->d_ok, ZG_NODE_CHUNK) == hipSuccess && dalloc(&ctx->d_out, ZG_NODE_CHUNK) == hipSuccess;
-  for (int i = 0; ok && i < 5; i++) ok = hipEventCreate(&ctx->ev[i]) == hipSuccess;
+  for (int i = 0; ok && i < ZG_NEV; i++) ok = hipEventCreate(&ctx->ev[i]) == hipSuccess;
   ok = ok && hipMemset(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS) == hipSuccess;
   if (!ok) {
     zg_destroy(ctx);
@@ -121,9 +126,10 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out};
   for (void* p : ptrs)
     if (p) hipFree(p);
-  for (int i = 0; i < 5; i++)
+  for (int i = 0; i < ZG_NEV; i++)
     if (ctx->ev[i]) hipEventDestroy(ctx->ev[i]);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  if (ctx->side) hipStreamDestroy(ctx->side);
   delete ctx;
 }
 
@@ -357,21 +363,50 @@ static BatchBufs batch_bufs(zg_ctx* ctx) {
   return b;
 }
 
-// the pipeline on device-resident inputs already in ctx buffers
+static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs& nb, hipStream_t st) {
+  hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS)), dim3(ZG_BLOCK),
+                     0, st, b, nb);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, st, b, nb);
+  HIPCHK(hipGetLastError());
+  return ZG_OK;
+}
+
+// The pipeline on device-resident inputs already in ctx buffers.
+//   main stream: decode -> Miller -> Fq12 product tree
+//   side stream: (after decode) C / Fr sum trees -> root VK-side MSM -> root VK Miller loops
+// The side stream only needs the decode results, so its serial, few-thread work overlaps the
+// full-GPU Miller kernel instead of extending the critical path.
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
+  static const int root = 1;
+  HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   hipLaunchKernelGGL(k_batch_decode, dim3(nblocks(ctx->npad)), dim3(ZG_BLOCK), 0, ctx->stream, b);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  // side stream
+  HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
+  HIPCHK(hipEventRecord(ctx->ev[5], ctx->side));
+  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
+    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo);
+    HIPCHK(hipGetLastError());
+  }
+  NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
+  int rc = launch_node_msm_pairs(ctx, b, nb, ctx->side);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[6], ctx->side));
+  // main stream
   hipLaunchKernelGGL(k_batch_miller, dim3(nblocks(ctx->npad)), dim3(ZG_BLOCK), 0, ctx->stream, b);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_level, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
+    hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // trees + root pairs complete
+  ctx->root_pairs_ready = 1;
   return ZG_OK;
 }
 
@@ -385,6 +420,7 @@ static int check_kinds(zg_ctx* ctx, size_t n, const uint8_t* kinds) {
 
 static int begin_common(zg_ctx* ctx, size_t n) {
   if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
+  ctx->root_pairs_ready = 0;
   ctx->n = n;
   size_t npad = 1;
   while (npad < n) npad <<= 1;
@@ -455,17 +491,18 @@ extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs
 static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std::vector<int>* ok, uint8_t* out_bytes) {
   BatchBufs b = batch_bufs(ctx);
   if (ok) ok->assign(nodes.size(), 0);
+  // the root's VK-side MSM + pairs were computed by the pipeline on the side stream
+  const bool reuse_root = ctx->root_pairs_ready && nodes.size() == 1 && nodes[0] == 1;
   for (size_t off = 0; off < nodes.size(); off += ZG_NODE_CHUNK) {
     int m = (int)std::min((size_t)ZG_NODE_CHUNK, nodes.size() - off);
-    HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
     NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, m};
-    hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)m * ZG_NKINDS * ZG_MSM_SLOTS)), dim3(ZG_BLOCK), 0,
-                       ctx->stream, b, nb);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_node_pairs, dim3(nblocks((size_t)m * ZG_NKINDS * ZG_NPAIRS)), dim3(ZG_BLOCK), 0,
-                       ctx->stream, b, nb);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_node_final, dim3(nblocks(m)), dim3(ZG_BLOCK), 0, ctx->stream, b, nb, mode);
+    if (!reuse_root) {
+      ctx->root_pairs_ready = 0;  // d_msm / d_pairf are about to be overwritten
+      HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
+      int rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_node_final, dim3(m), dim3(64), 0, ctx->stream, b, nb, mode);
     HIPCHK(hipGetLastError());
     if (ok) HIPCHK(hipMemcpyAsync(ok->data() + off, ctx->d_ok, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));
     if (out_bytes) {
@@ -487,6 +524,8 @@ extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   for (int i = 0; i < 4; i++) hipEventElapsedTime(&ctx->timings[i], ctx->ev[i], ctx->ev[i + 1]);
+  hipEventElapsedTime(&ctx->timings[4], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
+  hipEventElapsedTime(&ctx->timings[5], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
   return rc;
 }
 
@@ -498,7 +537,7 @@ extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, i
   hipLaunchKernelGGL(k_f12_from_bytes, dim3(nblocks(count)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_bytes, (int)count,
                      ctx->d_pairf);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(1), 0, ctx->stream, ctx->d_pairf, (int)count, ctx->d_ok,
+  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(64), 0, ctx->stream, ctx->d_pairf, (int)count, ctx->d_ok,
                      ctx->d_out);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ok, ctx->d_ok, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -575,9 +614,9 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
   return zg_batch_finish(ctx, ok, status);
 }
 
-extern "C" int zg_last_timings(zg_ctx* ctx, float* ms4) {
-  if (!ctx || !ms4) return ZG_E_INVAL;
-  for (int i = 0; i < 4; i++) ms4[i] = ctx->timings[i];
+extern "C" int zg_last_timings(zg_ctx* ctx, float* ms6) {
+  if (!ctx || !ms6) return ZG_E_INVAL;
+  for (int i = 0; i < 6; i++) ms6[i] = ctx->timings[i];
   return ZG_OK;
 }
 

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "zg_constants.h"
+#include "zg_fq_asm.h"
 
 #define ZG_HD __host__ __device__
 #define ZG_INL __host__ __device__ __forceinline__
@@ -196,7 +197,12 @@ ZG_NOINL inline u32x16 fq_mul_v(u32x8 a0, u32x4 a1, u32x8 b0, u32x4 b1) {
     a.l[8 + i] = a1[i];
     b.l[8 + i] = b1[i];
   }
-  Fq r = fp_mul_inl<FqM>(a, b);
+  Fq r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  fq_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning
+#else
+  r = fp_mul_inl<FqM>(a, b);   // host build of the test harness (tests/native): portable CIOS
+#endif
   u32x16 o;
 #pragma unroll
   for (int i = 0; i < 12; i++) o[i] = r.l[i];
@@ -274,7 +280,73 @@ ZG_INL Fq fq_pow_limbs(const Fq& a, const uint32_t* e, int nbits) {
   return r;
 }
 
-ZG_INL Fq fq_inv(const Fq& a) { return fq_pow_limbs(a, FQ_EXP_INV, 381); }
+// Variable-time inverse (binary extended Euclid) of a Montgomery-form element: public data
+// only. Returns the Montgomery form of the inverse. a != 0.
+ZG_NOINL inline Fq fq_inv_vartime(Fq a) {
+  if (fq_is_zero(a)) return a;  // never reached for a Miller product; guards the loop
+  Fq u = a, v, x1 = fp_zero<FqM>(), x2 = fp_zero<FqM>();
+  for (int i = 0; i < 12; i++) v.l[i] = FQ_P[i];
+  x1.l[0] = 1;
+  auto is_one = [](const Fq& z) {
+    uint32_t acc = z.l[0] ^ 1u;
+    for (int i = 1; i < 12; i++) acc |= z.l[i];
+    return acc == 0;
+  };
+  auto half = [](Fq& x) {  // x = x / 2 mod p  (x < p)
+    uint32_t c = 0;
+    if (x.l[0] & 1u) {
+      for (int i = 0; i < 12; i++) {
+        uint64_t s = (uint64_t)x.l[i] + FQ_P[i] + c;
+        x.l[i] = (uint32_t)s;
+        c = (uint32_t)(s >> 32);
+      }
+    }
+    for (int i = 0; i < 11; i++) x.l[i] = (x.l[i] >> 1) | (x.l[i + 1] << 31);
+    x.l[11] = (x.l[11] >> 1) | (c << 31);
+  };
+  auto shr1 = [](Fq& x) {
+    for (int i = 0; i < 11; i++) x.l[i] = (x.l[i] >> 1) | (x.l[i + 1] << 31);
+    x.l[11] >>= 1;
+  };
+  while (!is_one(u) && !is_one(v)) {
+    while (!(u.l[0] & 1u)) {
+      shr1(u);
+      half(x1);
+    }
+    while (!(v.l[0] & 1u)) {
+      shr1(v);
+      half(x2);
+    }
+    // u >= v ?
+    uint32_t borrow = 0;
+    Fq d;
+    for (int i = 0; i < 12; i++) {
+      uint64_t t = (uint64_t)u.l[i] - v.l[i] - borrow;
+      d.l[i] = (uint32_t)t;
+      borrow = (uint32_t)(t >> 63);
+    }
+    if (!borrow) {
+      u = d;
+      x1 = fq_sub(x1, x2);
+    } else {
+      uint32_t b2 = 0;
+      for (int i = 0; i < 12; i++) {
+        uint64_t t = (uint64_t)v.l[i] - u.l[i] - b2;
+        v.l[i] = (uint32_t)t;
+        b2 = (uint32_t)(t >> 63);
+      }
+      x2 = fq_sub(x2, x1);
+    }
+  }
+  Fq inv_plain = is_one(u) ? x1 : x2;       // (aR)^-1 as an integer mod p
+  return fq_mul(inv_plain, fq_const(FQ_R3));  // (aR)^-1 * R^3 / R = a^-1 R
+}
+
+
+// Every inversion on this path is of public data (proofs, keys, batch products).
+ZG_INL Fq fq_inv(const Fq& a) { return fq_inv_vartime(a); }
+// constant-time Fermat inverse (kept for reference / tests)
+ZG_INL Fq fq_inv_fermat(const Fq& a) { return fq_pow_limbs(a, FQ_EXP_INV, 381); }
 
 // Returns true and sets *out if a is a square (pairing Fq::sqrt: p = 3 mod 4).
 ZG_INL bool fq_sqrt(const Fq& a, Fq* out) {

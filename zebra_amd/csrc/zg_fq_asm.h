@@ -5,9 +5,9 @@
 // (The compiler's own lowering of the same C needs 4-5 instructions per MAC: it cannot
 // use the mad's carry-out.)
 #pragma once
-#include "zg_constants.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "zg_constants.h"
 
 namespace zg {
 

@@ -23,6 +23,16 @@ enum : uint8_t {
 #define ZG_MAX_IC 10
 #define ZG_MAX_INPUTS 9
 #define ZG_NKINDS 3
+#define ZG_SHIFTS 8  // 255-bit scalars as 8 x 32-bit chunks
+
+// [2^(32 w)] p for w = 0..7 (affine)
+ZG_NOINL inline void g1_shift_table(const G1A& p, G1A* out) {
+  G1J cur = jac_from_aff(p);
+  for (int w = 0; w < ZG_SHIFTS; w++) {
+    out[w] = jac_to_aff(cur);
+    for (int d = 0; d < 32; d++) cur = jac_dbl(cur);
+  }
+}
 
 // A prepared verifying key, resident in HBM.
 struct DevVK {
@@ -35,6 +45,10 @@ struct DevVK {
   Line neg_gamma_lines[ZG_NCOEFF]; // G2Prepared(-gamma)
   Line neg_delta_lines[ZG_NCOEFF]; // G2Prepared(-delta)
   Line beta_lines[ZG_NCOEFF];      // G2Prepared(beta)  (batch alpha/beta term)
+  // fixed-base tables for the batch's VK-side MSM: [2^(32 w)] ic[j] and [2^(32 w)] alpha,
+  // so a 255-bit scalar multiplication splits into 8 independent 32-bit ones
+  G1A ic_sh[ZG_MAX_IC][ZG_SHIFTS];
+  G1A alpha_sh[ZG_SHIFTS];
 };
 
 // Raw uncompressed VK as uploaded by the host (crypto/src/json/groth16.rs:33-49 fields).
@@ -67,6 +81,8 @@ ZG_NOINL inline int vk_prepare(const RawVK& raw, DevVK* vk) {
   if (!ng.inf) g2_prepare(ng, vk->neg_gamma_lines);
   if (!nd.inf) g2_prepare(nd, vk->neg_delta_lines);
   if (!vk->beta.inf) g2_prepare(vk->beta, vk->beta_lines);
+  for (int i = 0; i < raw.n_ic; i++) g1_shift_table(vk->ic[i], vk->ic_sh[i]);
+  g1_shift_table(vk->alpha, vk->alpha_sh);
   vk->loaded = 1;
   return 0;
 }

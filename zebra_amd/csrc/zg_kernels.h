@@ -9,6 +9,7 @@
 // (heap layout, leaves at npad + i) so any contiguous node can be re-checked exactly:
 // bisection on failure re-uses them.
 #pragma once
+#include "zg_coop.h"
 #include "zg_groth16.h"
 
 namespace zg {
@@ -87,12 +88,20 @@ __global__ void __launch_bounds__(64) k_batch_miller(BatchBufs b) {
   b.ftree[b.npad + i] = f;
 }
 
-// product-tree level: nodes [lo, 2 lo)
-__global__ void __launch_bounds__(64) k_tree_level(BatchBufs b, int lo) {
+// Fq12 product-tree level: nodes [lo, 2 lo)
+__global__ void __launch_bounds__(64) k_tree_f(BatchBufs b, int lo) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= lo) return;
+  const int node = lo + j;
+  b.ftree[node] = f12_mul(b.ftree[2 * node], b.ftree[2 * node + 1]);
+}
+
+// C-sum and Fr scalar-sum tree level (depends on k_batch_decode only, so it runs on the
+// side stream concurrently with the Miller kernel)
+__global__ void __launch_bounds__(64) k_tree_cs(BatchBufs b, int lo) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= lo) return;
   const int node = lo + j, l = 2 * node, r = 2 * node + 1;
-  b.ftree[node] = f12_mul(b.ftree[l], b.ftree[r]);
   for (int k = 0; k < ZG_NKINDS; k++) {
     b.ctree[node * ZG_NKINDS + k] = jac_add(b.ctree[l * ZG_NKINDS + k], b.ctree[r * ZG_NKINDS + k]);
     for (int m = 0; m < ZG_MAX_IC; m++)
@@ -110,13 +119,15 @@ struct NodeBufs {
   int m;
 };
 
-// VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k
+// VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k, each 255-bit scalar
+// split into 8 x 32-bit chunks against the pre-shifted bases [2^(32 w)] base (8 threads).
 __global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nb.m * ZG_NKINDS * ZG_MSM_SLOTS) return;
-  const int idx = t / (ZG_NKINDS * ZG_MSM_SLOTS);
-  const int kind = (t / ZG_MSM_SLOTS) % ZG_NKINDS;
-  const int j = t % ZG_MSM_SLOTS;
+  if (t >= nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS) return;
+  const int w = t % ZG_SHIFTS;
+  const int j = (t / ZG_SHIFTS) % ZG_MSM_SLOTS;
+  const int kind = (t / (ZG_SHIFTS * ZG_MSM_SLOTS)) % ZG_NKINDS;
+  const int idx = t / (ZG_SHIFTS * ZG_MSM_SLOTS * ZG_NKINDS);
   const int node = nb.nodes[idx];
   const DevVK& vk = b.vks[kind];
   G1J res = jac_infinity<Fq>();
@@ -124,75 +135,132 @@ __global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb) {
     const Fr* s = b.stree + (node * ZG_NKINDS + kind) * ZG_MAX_IC;
     if (j < vk.ic_len) {
       Fr sc = fr_from_mont(s[j]);
-      res = jac_mul_limbs(vk.ic[j], sc.l, 255);
+      res = jac_mul_limbs(vk.ic_sh[j][w], &sc.l[w], 32);
     } else if (j == ZG_MAX_IC && !vk.alpha.inf) {
       Fr sc = fr_from_mont(fp_neg<FrM>(s[0]));
-      res = jac_mul_limbs(vk.alpha, sc.l, 255);
+      res = jac_mul_limbs(vk.alpha_sh[w], &sc.l[w], 32);
     }
   }
   nb.msm[t] = res;
 }
 
-// VK-side Miller loops per checked node, with the prepared lines of the VK
+// slot[dst] = the sparse line c2 + (c1 px) v + (c0 py) v w as an Fq12 (pairing `ell` operand)
+__device__ void coop_line(CoopWS* ws, int dst, const Line& c, const Fq& px, const Fq& py) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 12) {
+    Fq v = fp_zero<FqM>();
+    if (lane == 0) v = c.c2.c0;
+    if (lane == 1) v = c.c2.c1;
+    if (lane == 2) v = fq_mul(c.c1.c0, px);
+    if (lane == 3) v = fq_mul(c.c1.c1, px);
+    if (lane == 8) v = fq_mul(c.c0.c0, py);
+    if (lane == 9) v = fq_mul(c.c0.c1, py);
+    ws->slot[dst][lane] = v;
+  }
+  __syncthreads();
+}
+
+// Bls12::miller_loop of one pair with prepared lines, on the cooperative engine -> slot 0
+__device__ void coop_miller_prepared(CoopWS* ws, const Fq& px, const Fq& py, const Line* coeffs) {
+  coop_set_one(ws, 0);
+  int n = 0;
+  for (int i = ZG_XH_TOP; i >= 0; i--) {
+    coop_line(ws, 1, coeffs[n++], px, py);
+    coop_mul(ws, 0, 0, 1);
+    if ((ZG_XH >> i) & 1ull) {
+      coop_line(ws, 1, coeffs[n++], px, py);
+      coop_mul(ws, 0, 0, 1);
+    }
+    coop_mul(ws, 0, 0, 0);
+  }
+  coop_line(ws, 1, coeffs[n++], px, py);
+  coop_mul(ws, 0, 0, 1);
+  coop_conj(ws, 0, 0);
+}
+
+// VK-side Miller loops per checked node: one wave per (node, kind, pair)
 __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ CoopWS ws;
+  __shared__ Fq px, py;
+  __shared__ const Line* lines;
+  const int t = blockIdx.x;
   if (t >= nb.m * ZG_NKINDS * ZG_NPAIRS) return;
   const int idx = t / (ZG_NKINDS * ZG_NPAIRS);
   const int kind = (t / ZG_NPAIRS) % ZG_NKINDS;
   const int pair = t % ZG_NPAIRS;
   const int node = nb.nodes[idx];
   const DevVK& vk = b.vks[kind];
-  Fq12 f = f12_one();
-  if (vk.loaded) {
-    const G1J* ms = nb.msm + (idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS;
-    G1J pj = jac_infinity<Fq>();
-    const Line* lines = nullptr;
-    if (pair == 0 && !vk.gamma.inf) {
-      for (int j = 0; j < vk.ic_len; j++) pj = jac_add(pj, ms[j]);
-      lines = vk.neg_gamma_lines;
-    } else if (pair == 1 && !vk.delta.inf) {
-      pj = b.ctree[node * ZG_NKINDS + kind];
-      lines = vk.neg_delta_lines;
-    } else if (pair == 2 && !vk.beta.inf) {
-      pj = ms[ZG_MAX_IC];
-      lines = vk.beta_lines;
-    }
-    if (lines) {
-      G1A p = jac_to_aff(pj);
-      if (!p.inf) f = miller_loop_prepared(p, lines);
+  if (threadIdx.x == 0) {
+    lines = nullptr;
+    if (vk.loaded) {
+      const G1J* ms = nb.msm + (size_t)(idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS * ZG_SHIFTS;
+      G1J pj = jac_infinity<Fq>();
+      const Line* ln = nullptr;
+      if (pair == 0 && !vk.gamma.inf) {
+        for (int j = 0; j < vk.ic_len * ZG_SHIFTS; j++) pj = jac_add(pj, ms[j]);
+        ln = vk.neg_gamma_lines;
+      } else if (pair == 1 && !vk.delta.inf) {
+        pj = b.ctree[node * ZG_NKINDS + kind];
+        ln = vk.neg_delta_lines;
+      } else if (pair == 2 && !vk.beta.inf) {
+        for (int w = 0; w < ZG_SHIFTS; w++) pj = jac_add(pj, ms[ZG_MAX_IC * ZG_SHIFTS + w]);
+        ln = vk.beta_lines;
+      }
+      if (ln) {
+        G1A p = jac_to_aff(pj);
+        if (!p.inf) {
+          px = p.x;
+          py = p.y;
+          lines = ln;
+        }
+      }
     }
   }
-  nb.pairf[t] = f;
+  __syncthreads();
+  if (lines) {
+    coop_miller_prepared(&ws, px, py, lines);
+  } else {
+    coop_set_one(&ws, 0);
+  }
+  coop_store(&ws, 0, nb.pairf[t]);
 }
 
+// One wave per node (lane-cooperative Fq12 engine, zg_coop.h).
 // mode 0: FE(product) == 1 -> ok ; mode 1: write product (Miller partial) ;
 // mode 2: FE(product without the alpha/beta pairs) -> out (accumulated GT)
 __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int mode) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ CoopWS ws;
+  const int idx = blockIdx.x;
   if (idx >= nb.m) return;
-  Fq12 f = b.ftree[nb.nodes[idx]];
+  coop_load(&ws, 0, b.ftree[nb.nodes[idx]]);
   for (int k = 0; k < ZG_NKINDS; k++)
     for (int p = 0; p < ZG_NPAIRS; p++) {
       if (mode == 2 && p == 2) continue;
-      f = f12_mul(f, nb.pairf[(idx * ZG_NKINDS + k) * ZG_NPAIRS + p]);
+      coop_load(&ws, 1, nb.pairf[(idx * ZG_NKINDS + k) * ZG_NPAIRS + p]);
+      coop_mul(&ws, 0, 0, 1);
     }
   if (mode == 1) {
-    nb.out[idx] = f;
+    coop_store(&ws, 0, nb.out[idx]);
     return;
   }
-  Fq12 g = final_exponentiation(f);
-  if (mode == 2) nb.out[idx] = g;
-  nb.ok[idx] = f12_is_one(g) ? 1 : 0;
+  coop_final_exp(&ws, 0, 0);
+  if (mode == 2) coop_store(&ws, 0, nb.out[idx]);
+  const bool one = coop_is_one(&ws, 0);
+  if (threadIdx.x == 0) nb.ok[idx] = one ? 1 : 0;
 }
 
-// K7 across ranks: product of partials, one final exponentiation, == 1 ?
-__global__ void k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
-  if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
-  Fq12 f = f12_one();
-  for (int c = 0; c < count; c++) f = f12_mul(f, parts[c]);
-  Fq12 g = final_exponentiation(f);
-  *gt = g;
-  *ok = f12_is_one(g) ? 1 : 0;
+// K7 across ranks: product of partials, ONE final exponentiation (one wave), == 1 ?
+__global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
+  __shared__ CoopWS ws;
+  coop_load(&ws, 0, parts[0]);
+  for (int c = 1; c < count; c++) {
+    coop_load(&ws, 1, parts[c]);
+    coop_mul(&ws, 0, 0, 1);
+  }
+  coop_final_exp(&ws, 0, 0);
+  coop_store(&ws, 0, *gt);
+  const bool one = coop_is_one(&ws, 0);
+  if (threadIdx.x == 0) *ok = one ? 1 : 0;
 }
 
 __global__ void k_f12_to_bytes(const Fq12* a, int count, uint8_t* out) {

@@ -171,7 +171,7 @@ class Context:
         return list(st.raw[:n])
 
     def last_timings(self):
-        a = (ctypes.c_float * 4)()
+        a = (ctypes.c_float * 6)()
         self._chk(lib().zg_last_timings(self._p, a))
         return list(a)
 
