@@ -11,6 +11,7 @@
 #pragma once
 #include "zg_coop.h"
 #include "zg_groth16.h"
+#include "zg_prog.h"
 
 namespace zg {
 
@@ -86,6 +87,115 @@ __global__ void __launch_bounds__(64) k_batch_miller(BatchBufs b) {
   Fq12 f = f12_one();
   if (i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf) f = miller_loop_1(b.ptA[i], b.ptB[i]);
   b.ftree[b.npad + i] = f;
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-proof Miller loop as two staged programs (zg_prog.h; lane = proof, wave = product):
+//   k_batch_lines : the R-chain (pairing's G2Prepared steps for B_i, with the ell scaling
+//                   by r_i A_i folded in) -> 68 line triples per proof in HBM
+//   k_batch_fchain: the f-chain (sparse line products + squarings) -> ftree leaves
+// A block = 64 proofs; NW waves share each stage's independent Fq2 products.
+#define ZG_LINES_NW 6      // widest stage of dbl/add
+#define ZG_LINES_ATOMS 24  // X Y Z QX QY PX PY + up to 17 products
+#define ZG_FC_NW 12        // 3 waves per SIMD (168 VGPRs); m014 has 13 products -> 2 rounds
+#define ZG_FC_ATOMS 22     // f0..f5 A B C + up to 13 products
+#define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
+
+__device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
+  return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
+}
+
+// lines layout: [step][proof][A, B, C]
+__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines, uint4* wsbuf) {
+  __shared__ uint4 lds_atoms[ZG_LINES_ATOMS * ZG_ATOM_ROWS * 64];  // 144 KB
+  const AtomSpace at{lds_atoms};
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int proof = blockIdx.x * 64 + lane;
+  const bool act = proof_active(b, proof);
+  if (wave == 0) {
+    G2A q;
+    G1A p;
+    if (act) {
+      q = b.ptB[proof];
+      p = b.ptA[proof];
+    } else {
+      q.x = q.y = f2_one();
+      p.x = p.y = fq_one();
+    }
+    at.put(0, q.x);
+    at.put(1, q.y);
+    at.put(2, f2_one());
+    at.put(3, q.x);
+    at.put(4, q.y);
+    at.put(5, {p.x, fp_zero<FqM>()});
+    at.put(6, {p.y, fp_zero<FqM>()});
+  }
+  __syncthreads();
+  int n = 0;
+  for (int i = ZG_XH_TOP; i >= -1; i--) {
+    for (int pass = 0; pass < 2; pass++) {
+      if (pass == 1 && (i < 0 || !((ZG_XH >> i) & 1ull))) break;
+      const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
+      prog_run_stages(pid, at, ZG_LINES_NW);
+      const Fq2 v = prog_out(pid, at, wave);
+      __syncthreads();
+      if (wave < 3)
+        at.put(wave, v);
+      else if (proof < b.npad)
+        lines[((size_t)n * b.npad + proof) * 3 + (wave - 3)] = act ? v : f2_one();
+      __syncthreads();
+      n++;
+    }
+  }
+}
+
+__device__ __forceinline__ void fchain_step(const BatchBufs& b, const AtomSpace& at, const Fq2* lines, int n, int pid) {
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int proof = blockIdx.x * 64 + lane;
+  if (pid == ZG_PROG_M014) {
+    if (wave < 3) at.put(6 + wave, proof < b.npad ? lines[((size_t)n * b.npad + proof) * 3 + wave] : f2_one());
+    __syncthreads();
+  }
+  prog_run_stages(pid, at, ZG_FC_NW);
+  Fq2 v;
+  if (wave < 6) v = prog_out(pid, at, wave);
+  __syncthreads();
+  if (wave < 6) at.put(wave, v);
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines, uint4* wsbuf) {
+  __shared__ uint4 lds_atoms[ZG_FC_ATOMS * ZG_ATOM_ROWS * 64];  // 132 KB
+  const AtomSpace at{lds_atoms};
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int proof = blockIdx.x * 64 + lane;
+  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  __syncthreads();
+  // one call site (a runtime, wave-uniform program id) keeps the engine's code single-copy:
+  // per bit i: f *= dbl line; [f *= add line]; f = f^2 -- then the last dbl line.
+  int n = 0;
+  for (int i = ZG_XH_TOP, ph = 0;;) {
+    const int pid = wave_uniform(ph == 2 ? ZG_PROG_SQR : ZG_PROG_M014);
+    fchain_step(b, at, lines, n, pid);
+    if (i < 0) break;
+    if (ph == 0) {
+      ph = ((ZG_XH >> i) & 1ull) ? 1 : 2;
+      n++;
+    } else if (ph == 1) {
+      ph = 2;
+      n++;
+    } else {
+      ph = 0;
+      i--;
+    }
+  }
+  // conjugate (u < 0) and store the leaf; inactive / padding proofs contribute 1
+  if (wave < 6 && proof < b.npad) {
+    Fq2 v = at.get(wave);
+    if (wave >= 3) v = f2_neg(v);
+    if (!proof_active(b, proof)) v = wave == 0 ? f2_one() : f2_zero();
+    reinterpret_cast<Fq2*>(&b.ftree[b.npad + proof])[wave] = v;
+  }
 }
 
 // Fq12 product-tree level: nodes [lo, 2 lo)
