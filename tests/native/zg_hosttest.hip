@@ -2,6 +2,7 @@
 // on the CPU so the CPU-only test tier can check it against the oracle without a GPU.
 // Never linked into, or loaded by, the product library.
 #include <string.h>
+#include "../../zebra_amd/csrc/zg_coop.h"
 #include "../../zebra_amd/csrc/zg_groth16.h"
 
 using namespace zg;
@@ -96,6 +97,20 @@ int zgt_verify_single(const uint8_t* proof, const uint8_t* inputs, int k, uint8_
   uint8_t st = verify_single(g_vk, proof, inputs, k, &g);
   if (st == ST_OK || st == ST_VERIFY_FAILED) f12_to_bytes(g, gt);
   return st;
+}
+
+// lazy linear form of the cooperative engine: sum_t c_t x_t mod p for raw 384-bit limbs x_t
+// (little-endian 32-bit words, 12 per value); returns the result's limbs
+void zgt_lazy_form(const uint32_t* xs, const int* cs, int n, int canon, uint32_t* out) {
+  LazyAcc a;
+  lazy_zero(a);
+  for (int t = 0; t < n; t++) {
+    Fq x;
+    for (int i = 0; i < 12; i++) x.l[i] = xs[12 * t + i];
+    lazy_term(a, x, cs[t]);
+  }
+  Fq r = lazy_finish(a, canon != 0);
+  for (int i = 0; i < 12; i++) out[i] = r.l[i];
 }
 
 }  // extern "C"

@@ -68,8 +68,13 @@ def test_f12_ops(L):
 def test_f2_sqrt(L):
     rng = random.Random(4)
     out = hostlib.buf(96)
-    for _ in range(6):
-        a = (rng.randrange(P), rng.randrange(P))
+    cases = [(rng.randrange(P), rng.randrange(P)) for _ in range(40)]
+    # a in Fq (both branches: a0 a square / -a0 a square), zero, pure imaginary, squares of x + 0u / 0 + xu
+    cases += [(rng.randrange(P), 0) for _ in range(6)] + [(0, 0), (0, rng.randrange(P)), (P - 1, 0), (1, 0)]
+    for _ in range(4):
+        x = rng.randrange(P)
+        cases += [B.f2_sqr((x, 0)), B.f2_sqr((0, x)), B.f2_sqr((x, rng.randrange(P)))]
+    for a in cases:
         ok = L.zgt_f2_sqrt(fq_b(a[0]) + fq_b(a[1]), out)
         want = B.f2_sqrt(a)
         assert bool(ok) == (want is not None)
@@ -116,3 +121,29 @@ def test_subgroup_checks(L):
         n2 += 1
         assert L.zgt_g2_in_subgroup(b"".join(fq_b(v) for v in (x[0], x[1], y[0], y[1]))) == int(
             B.g2_in_subgroup((x, y)))
+
+
+def test_lazy_linear_forms(L):
+    """zg_coop.h LazyAcc: any 384-bit terms, |c| < 128, <= 8 terms -> value mod p, < 2.2p
+    (canon: < p); the extremes of the bounds included."""
+    import ctypes
+    rng = random.Random(8)
+    out = (ctypes.c_uint32 * 12)()
+    top = (1 << 384) - 1
+    for it in range(400):
+        n = rng.randrange(1, 9)
+        if it % 4 == 0:
+            xs = [top] * n
+            cs = [rng.choice((-127, 127)) for _ in range(n)]
+        else:
+            xs = [rng.choice((rng.randrange(P), rng.randrange(1 << 384), rng.randrange(3 * P))) % (1 << 384)
+                  for _ in range(n)]
+            cs = [rng.randrange(-127, 128) for _ in range(n)]
+        xa = (ctypes.c_uint32 * (12 * n))(*[(x >> (32 * i)) & 0xFFFFFFFF for x in xs for i in range(12)])
+        ca = (ctypes.c_int * n)(*cs)
+        want = sum(c * x for c, x in zip(cs, xs)) % P
+        for canon in (0, 1):
+            L.zgt_lazy_form(xa, ca, n, canon, out)
+            got = sum(int(out[i]) << (32 * i) for i in range(12))
+            assert got % P == want
+            assert got < (P if canon else (22 * P) // 10)

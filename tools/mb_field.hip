@@ -14,13 +14,19 @@ using namespace zg;
 template <int MODE>
 __global__ void __launch_bounds__(256) k_mul(const Fq* in, Fq* out, int iters) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  Fq x = in[i], y = in[i + 1];
+  Fq x = in[i], y = in[i + 1], z = in[i + 2];
   for (int k = 0; k < iters; k++) {
     if (MODE == 0)
       x = fp_mul_inl<FqM>(x, y);
-    else
+    else if (MODE == 1)
       fq_mul_fips(x.l, x.l, y.l);
+    else {  // two independent chains per lane (ILP 2), each counts as one mul per iteration
+      fq_mul_fips(x.l, x.l, y.l);
+      fq_mul_fips(z.l, z.l, y.l);
+    }
   }
+  if (MODE == 2)
+    for (int w = 0; w < 12; w++) x.l[w] ^= z.l[w];
   out[i] = x;
 }
 
@@ -34,7 +40,7 @@ __global__ void __launch_bounds__(256) k_mul(const Fq* in, Fq* out, int iters) {
   } while (0)
 
 int main() {
-  const int maxthreads = 256 * 256 * 8 + 1;
+  const int maxthreads = 256 * 256 * 8 + 2;
   Fq* h = (Fq*)malloc(sizeof(Fq) * maxthreads);
   srand(1);
   for (int i = 0; i < maxthreads; i++) {
@@ -63,7 +69,7 @@ int main() {
   printf("asm vs C mismatches: %d\n", bad);
   const int iters = 512;
   int waves_per_simd[] = {1, 2, 4, 8};
-  for (int mode = 0; mode < 2; mode++) {
+  for (int mode = 0; mode < 3; mode++) {
     for (int wi = 0; wi < 4; wi++) {
       int wps = waves_per_simd[wi];
       int blocks = 256 * wps;  // 256 threads = 4 waves = 1 per SIMD per block
@@ -71,19 +77,21 @@ int main() {
         CK(hipEventRecord(e0));
         if (mode == 0)
           k_mul<0><<<blocks, 256>>>(din, dout, iters);
-        else
+        else if (mode == 1)
           k_mul<1><<<blocks, 256>>>(din, dout, iters);
+        else
+          k_mul<2><<<blocks, 256>>>(din, dout, iters);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        double muls = (double)blocks * 256 * iters;
+        double muls = (double)blocks * 256 * iters * (mode == 2 ? 2 : 1);
         double rate = muls / (ms * 1e-3);
         // cycles per Fq-mul per SIMD assuming 2.4 GHz: SIMDs = 1024, each wave = 64 muls in parallel
         double cyc = (ms * 1e-3) * 2.4e9 / ((double)iters * wps);
         if (rep == 1)
           printf("%s waves/SIMD=%d  %.3f ms  %.2f G Fq-mul/s  ~%.0f cycles per wave-Fq-mul (latency view)\n",
-                 mode ? "ASM" : "C  ", wps, ms, rate / 1e9, cyc);
+                 mode == 2 ? "ASM-ILP2" : mode ? "ASM" : "C  ", wps, ms, rate / 1e9, cyc);
       }
     }
   }

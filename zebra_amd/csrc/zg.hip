@@ -21,6 +21,7 @@ using namespace zg;
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 8
+#define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 
 struct zg_ctx {
   int device = 0;
@@ -410,7 +411,10 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
+    if (lo >= ZG_TREE_COOP_BELOW)
+      hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
+    else
+      hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));

@@ -4,9 +4,11 @@
 //
 // A single-lane Fq12 product is 54 dependent-in-program-order Fq multiplications; the
 // final exponentiation is ~15,600 of them in sequence, which on one lane is pure latency
-// (97 ms in round 1). Here an operation is   out_j = sum_k c_jk P_k + sum_i d_ji a_i  with
-// P_k = L_k(a, b) R_k(a, b) independent (tables from gen_coop.py): lanes 0..53 form their
-// operands and multiply (phase 1), lanes 0..11 combine (phase 2). Operands live in LDS.
+// (97 ms in round 1). Here an operation runs as levels of independent lane tasks (tables
+// from gen_coop.py): up to 54 Fq products on separate lanes, then the Karatsuba recombination
+// as levels of short linear forms (Fq2 products, Fq6 products, outputs). Linear forms are
+// evaluated branch-free with lazy reduction (LazyAcc): the lanes of a wave evaluate
+// different forms without diverging. Operands and the form tables live in LDS.
 #pragma once
 #include "zg_coop_tables.h"
 #include "zg_pairing.h"
@@ -15,65 +17,128 @@ namespace zg {
 
 #define ZG_COOP_SLOTS 8
 struct CoopWS {
-  Fq slot[ZG_COOP_SLOTS][12];  // Fq12 registers, coefficient order of f12_coeffs
-  Fq prod[64 + 12];            // products, then a copy of the input coefficients
+  Fq slot[ZG_COOP_SLOTS][12];       // Fq12 registers, coefficient order of f12_coeffs
+  Fq v[24 + ZG_COOP_MAXATOMS];      // op workspace: inputs a (0..11), b (12..23), then atoms
+  CoopForm forms[ZG_COOP_NFORMS];   // LDS copy of COOP_FORMS (per-lane table reads at LDS latency)
 };
 
-ZG_INL Fq fq_small_mul(const Fq& x, int c) {
-  Fq r = fp_zero<FqM>();
-  int m = c < 0 ? -c : c;
-  for (int i = 0; i < m; i++) r = fq_add(r, x);
-  return c < 0 ? fq_neg(r) : r;
+// Lazy linear forms  sum_t c_t x_t  (|c_t| < 128, <= 8 terms, x_t any 384-bit value):
+// one 64-bit accumulator per limb, no carry chain per term. A negative term adds
+// |c| * ~x  (= |c| (2^384 - 1 - x)), i.e. -|c| x + |c| - |c| 2^384; the per-lane count B of
+// such |c| is corrected once at the end by adding B + B (p - 2^384 mod p).
+struct LazyAcc {
+  uint64_t l[12];
+  uint32_t b;
+};
+ZG_INL void lazy_zero(LazyAcc& a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.l[i] = 0;
+  a.b = 0;
 }
-
-__device__ __forceinline__ Fq coop_lin(const CoopWS* ws, const CoopTerms& t, int a, int b) {
-  Fq acc = fp_zero<FqM>();
-  for (int q = 0; q < t.n; q++) {
-    const int v = t.t[q];
-    const int idx = v & 0xff, c = v >> 8;
-    const Fq& x = idx < 12 ? ws->slot[a][idx] : ws->slot[b][idx - 12];
-    if (c == 1)
-      acc = fq_add(acc, x);
-    else if (c == -1)
-      acc = fq_sub(acc, x);
-    else
-      acc = fq_add(acc, fq_small_mul(x, c));
+ZG_INL void lazy_term(LazyAcc& a, const Fq& x, int c) {
+  const uint32_t m = (uint32_t)(c < 0 ? -c : c);
+  const uint32_t neg = c < 0 ? 0xffffffffu : 0u;
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.l[i] += (uint64_t)(x.l[i] ^ neg) * m;  // v_xor + v_mad_u64_u32
+  a.b += m & neg;
+}
+// value mod p, < 2.2 p (a valid Montgomery-product operand); canon = true: < p
+ZG_INL Fq lazy_finish(const LazyAcc& a, bool canon) {
+  uint32_t w[13];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {  // carry-propagate (each l[i] < 2^42)
+    const uint64_t s = a.l[i] + c;
+    w[i] = (uint32_t)s;
+    c = s >> 32;
   }
-  return acc;
+  w[12] = (uint32_t)c;
+  uint64_t t = (uint64_t)w[0] + a.b;  // + B + B (p - 2^384 mod p)
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint64_t s = (uint64_t)a.b * FQ_NEG_R[i] + (i == 0 ? t : (uint64_t)w[i]) + c;
+    w[i] = (uint32_t)s;
+    c = s >> 32;
+  }
+  w[12] += (uint32_t)c;  // W < 2^395 < 2^14 p
+  // q = floor(float(W >> 352) * (1 - 2^-20) 2^352 / p): W/p - 1.2 < q <= W/p
+  const float top = (float)w[12] * 4294967296.0f + (float)w[11];
+  const uint32_t q = (uint32_t)(top * FQ_QSCALE);
+  Fq r;
+  uint32_t borrow = 0, carry = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint64_t qp = (uint64_t)q * FQ_P[i] + carry;
+    carry = (uint32_t)(qp >> 32);
+    const uint64_t d = (uint64_t)w[i] - (uint32_t)qp - borrow;
+    r.l[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  if (canon) r = fp_reduce_once<FqM>(fp_reduce_once<FqM>(r));
+  return r;
 }
 
-// slot[dst] = op(slot[a], slot[b]); dst may alias a or b.
-__device__ void coop_op(CoopWS* ws, int dst, int a, int b, const CoopTerms* L, const CoopTerms* R, const CoopOut* O,
-                        int np) {
+__device__ __forceinline__ Fq coop_form(const CoopWS* ws, int fi, bool canon) {
+  const CoopForm& f = ws->forms[fi];
+  LazyAcc acc;
+  lazy_zero(acc);
+  const int n = f.n;
+  for (int q = 0; q < n; q++) {
+    const int v = f.t[q];
+    lazy_term(acc, ws->v[v & 0xff], v >> 8);
+  }
+  return lazy_finish(acc, canon);
+}
+
+// copy the form tables into the block's LDS (once per kernel, before any coop op)
+__device__ void coop_init(CoopWS* ws) {
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(COOP_FORMS);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(ws->forms);
+  constexpr int nw = (int)(sizeof(CoopForm) * ZG_COOP_NFORMS / 2);
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+// slot[dst] = op(slot[a], slot[b]) for op = ZG_COOP_{MUL,SQR,CSQR,M014}; dst may alias a / b.
+// Level 0: one Fq product per lane; later levels: one linear form per lane; the last level
+// writes the 12 output coefficients.
+__device__ void coop_run(CoopWS* ws, int opid, int dst, int a, int b) {
   const int lane = threadIdx.x & 63;
-  if (lane < np) ws->prod[lane] = fq_mul(coop_lin(ws, L[lane], a, b), coop_lin(ws, R[lane], a, b));
-  if (lane < 12) ws->prod[64 + lane] = ws->slot[a][lane];
-  __syncthreads();
   if (lane < 12) {
-    Fq acc = fp_zero<FqM>();
-    const CoopOut& o = O[lane];
-    for (int q = 0; q < o.n; q++) {
-      const int v = o.t[q];
-      const int idx = v & 0xff, c = v >> 8;
-      const Fq& x = idx >= 32 ? ws->prod[idx - 32] : ws->prod[64 + idx];
-      if (c == 1)
-        acc = fq_add(acc, x);
-      else if (c == -1)
-        acc = fq_sub(acc, x);
-      else
-        acc = fq_add(acc, fq_small_mul(x, c));
-    }
-    ws->slot[dst][lane] = acc;
+    ws->v[lane] = ws->slot[a][lane];
+    ws->v[12 + lane] = ws->slot[b][lane];
   }
   __syncthreads();
+  const CoopOp& op = COOP_OPS[opid];
+  const int nlev = op.nlev;
+  int base = 24;
+  for (int l = 0; l < nlev; l++) {
+    const int cnt = op.cnt[l], off = op.off[l];
+    if (lane < cnt) {
+      if (l == 0) {
+        const Fq x = coop_form(ws, off + 2 * lane, false), y = coop_form(ws, off + 2 * lane + 1, false);
+        ws->v[base + lane] = fq_mul(x, y);
+      } else {
+        const Fq x = coop_form(ws, off + lane, l == nlev - 1);
+        if (l == nlev - 1)
+          ws->slot[dst][lane] = x;
+        else
+          ws->v[base + lane] = x;
+      }
+    }
+    base += cnt;
+    __syncthreads();
+  }
 }
 
-__device__ __forceinline__ void coop_mul(CoopWS* ws, int dst, int a, int b) {
-  coop_op(ws, dst, a, b, COOP_MUL_L, COOP_MUL_R, COOP_MUL_O, ZG_COOP_MUL_NP);
-}
+__device__ __forceinline__ void coop_mul(CoopWS* ws, int dst, int a, int b) { coop_run(ws, ZG_COOP_MUL, dst, a, b); }
+__device__ __forceinline__ void coop_sqr(CoopWS* ws, int dst, int a) { coop_run(ws, ZG_COOP_SQR, dst, a, a); }
 // squaring in the cyclotomic subgroup (Granger-Scott); only valid after the easy part
-__device__ __forceinline__ void coop_csqr(CoopWS* ws, int dst, int a) {
-  coop_op(ws, dst, a, a, COOP_CSQR_L, COOP_CSQR_R, COOP_CSQR_O, ZG_COOP_CSQR_NP);
+__device__ __forceinline__ void coop_csqr(CoopWS* ws, int dst, int a) { coop_run(ws, ZG_COOP_CSQR, dst, a, a); }
+// slot[dst] = slot[a] * line, the line in slot[b] as written by coop_line (mul_by_014)
+__device__ __forceinline__ void coop_mul014(CoopWS* ws, int dst, int a, int b) {
+  coop_run(ws, ZG_COOP_M014, dst, a, b);
 }
 
 __device__ __forceinline__ void coop_copy(CoopWS* ws, int dst, int a) {

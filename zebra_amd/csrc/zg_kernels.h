@@ -206,6 +206,18 @@ __global__ void __launch_bounds__(64) k_tree_f(BatchBufs b, int lo) {
   b.ftree[node] = f12_mul(b.ftree[2 * node], b.ftree[2 * node + 1]);
 }
 
+// the same level for small lo, one wave per node on the cooperative engine (latency-bound
+// levels near the root: a single-lane Fq12 product is 54 serial Fq products)
+__global__ void __launch_bounds__(64) k_tree_f_coop(BatchBufs b, int lo) {
+  __shared__ CoopWS ws;
+  coop_init(&ws);
+  const int node = lo + blockIdx.x;
+  coop_load(&ws, 0, b.ftree[2 * node]);
+  coop_load(&ws, 1, b.ftree[2 * node + 1]);
+  coop_mul(&ws, 0, 0, 1);
+  coop_store(&ws, 0, b.ftree[node]);
+}
+
 // C-sum and Fr scalar-sum tree level (depends on k_batch_decode only, so it runs on the
 // side stream concurrently with the Miller kernel)
 __global__ void __launch_bounds__(64) k_tree_cs(BatchBufs b, int lo) {
@@ -276,15 +288,15 @@ __device__ void coop_miller_prepared(CoopWS* ws, const Fq& px, const Fq& py, con
   int n = 0;
   for (int i = ZG_XH_TOP; i >= 0; i--) {
     coop_line(ws, 1, coeffs[n++], px, py);
-    coop_mul(ws, 0, 0, 1);
+    coop_mul014(ws, 0, 0, 1);
     if ((ZG_XH >> i) & 1ull) {
       coop_line(ws, 1, coeffs[n++], px, py);
-      coop_mul(ws, 0, 0, 1);
+      coop_mul014(ws, 0, 0, 1);
     }
-    coop_mul(ws, 0, 0, 0);
+    coop_sqr(ws, 0, 0);
   }
   coop_line(ws, 1, coeffs[n++], px, py);
-  coop_mul(ws, 0, 0, 1);
+  coop_mul014(ws, 0, 0, 1);
   coop_conj(ws, 0, 0);
 }
 
@@ -295,6 +307,7 @@ __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb) {
   __shared__ const Line* lines;
   const int t = blockIdx.x;
   if (t >= nb.m * ZG_NKINDS * ZG_NPAIRS) return;
+  coop_init(&ws);
   const int idx = t / (ZG_NKINDS * ZG_NPAIRS);
   const int kind = (t / ZG_NPAIRS) % ZG_NKINDS;
   const int pair = t % ZG_NPAIRS;
@@ -342,6 +355,7 @@ __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int
   __shared__ CoopWS ws;
   const int idx = blockIdx.x;
   if (idx >= nb.m) return;
+  coop_init(&ws);
   coop_load(&ws, 0, b.ftree[nb.nodes[idx]]);
   for (int k = 0; k < ZG_NKINDS; k++)
     for (int p = 0; p < ZG_NPAIRS; p++) {
@@ -362,6 +376,7 @@ __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int
 // K7 across ranks: product of partials, ONE final exponentiation (one wave), == 1 ?
 __global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
   __shared__ CoopWS ws;
+  coop_init(&ws);
   coop_load(&ws, 0, parts[0]);
   for (int c = 1; c < count; c++) {
     coop_load(&ws, 1, parts[c]);

@@ -69,26 +69,41 @@ ZG_INL Fq2 f2_pow_limbs(const Fq2& a, const uint32_t* e, int nbits) {
   f2_pow_limbs_p(&r, &a, e, nbits);
   return r;
 }
-// Square root in Fq2 (pairing Fq2::sqrt, Algorithm 9 of eprint 2012/685). Any root is
-// acceptable to the point decoders: they choose the sign afterwards.
+// Square root in Fq2 by the norm ("complex") method: two Fq exponentiations by (p-3)/4
+// instead of the two Fq2 exponentiations of pairing's Fq2::sqrt (Algorithm 9 of eprint
+// 2012/685); ~920 vs ~2,660 Fq multiplications. The decoders pick the sign of y from the
+// encoding flag afterwards, so which of the two roots is returned does not matter
+// (SURVEY.md 8(a) row a4). For a = a0 + a1 u with a1 != 0:
+//   g = sqrt(a0^2 + a1^2) (a is a square in Fq2 iff its norm is a square in Fq),
+//   d = (a0 + g)/2 != 0, e = d^((p-3)/4):
+//   d a square:  y = e d + (a1 e / 2) u          ((e d)^2 = d, 1/(e d) = e)
+//   otherwise :  y = a1 e / 2 - (e d) u          (-d is a square; (p-3)/4 is even)
 ZG_NOINL inline bool f2_sqrt(const Fq2& a, Fq2* out) {
-  if (f2_is_zero(a)) {
-    *out = a;
-    return true;
+  if (fq_is_zero(a.c1)) {  // a in Fq: sqrt(a0) or sqrt(-a0) u
+    const Fq e = fq_pow_pm3_4(a.c0);  // (-a0)^((p-3)/4) == e too: (p-3)/4 is even
+    const Fq s = fq_mul(e, a.c0);
+    if (fq_eq(fq_sqr(s), a.c0)) {
+      *out = {s, fp_zero<FqM>()};
+      return true;
+    }
+    const Fq t = fq_neg(s);  // e * (-a0)
+    *out = {fp_zero<FqM>(), t};
+    return fq_eq(fq_sqr(t), fq_neg(a.c0));
   }
-  Fq2 a1 = f2_pow_limbs(a, FQ_EXP_PM3_4, 379);
-  Fq2 alpha = f2_mul(f2_sqr(a1), a);
-  Fq2 a0 = f2_mul(f2_conj(alpha), alpha);
-  Fq2 neg1 = {fq_neg(fq_one()), fp_zero<FqM>()};
-  if (f2_eq(a0, neg1)) return false;
-  a1 = f2_mul(a1, a);
-  if (f2_eq(alpha, neg1)) {
-    *out = {fq_neg(a1.c1), a1.c0};  // a1 * u
-    return true;
-  }
-  alpha = f2_pow_limbs(f2_add(alpha, f2_one()), FQ_EXP_LEGENDRE, 380);
-  *out = f2_mul(a1, alpha);
-  return true;
+  const Fq n = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+  const Fq g = fq_mul(fq_pow_pm3_4(n), n);
+  if (!fq_eq(fq_sqr(g), n)) return false;
+  const Fq d = fq_half(fq_add(a.c0, g));
+  const Fq e = fq_pow_pm3_4(d);
+  const Fq ed = fq_mul(e, d);
+  const Fq h = fq_half(fq_mul(a.c1, e));
+  Fq2 y;
+  if (fq_eq(fq_sqr(ed), d))
+    y = {ed, h};
+  else
+    y = {h, fq_neg(ed)};
+  *out = y;
+  return f2_eq(f2_sqr(y), a);
 }
 
 // ------------------------------------------------------------------ Fq6
