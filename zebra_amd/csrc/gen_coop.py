@@ -218,7 +218,7 @@ def build(name, fn):
 
 def evaluate(op, a, b):
     env = {i: a[i] for i in range(12)}
-    env.update({12 + i: b[i] for i in range(12)})
+    env.update({12 + i: (b[i] if b else 0) for i in range(12)})
     k = NIN
     for li, forms in enumerate(op["levels"]):
         for fs in forms:

@@ -1,18 +1,27 @@
 #!/usr/bin/env python3
-"""Generate zg_prog_tables.h: Fq2-granularity staged programs for the multi-instance
-cooperative engine (zg_prog.h).
+"""Generate zg_prog_tables.h: the staged programs of the per-proof Miller loop (zg_prog.h),
+as round schedules, LDS slot maps and generated straight-line operand/output code.
 
-A program is a straight-line formula over Fq2 values (pairing 0.14.2's line doubling /
-addition steps with the `ell` scaling, the sparse line product mul_by_014, Fq12 squaring)
-run symbolically: every Fq2 multiplication becomes a *product* whose operands are linear
-forms, with Gaussian-integer coefficients (c0 + c1 u), over earlier atoms (program inputs or
-earlier products). Products are scheduled ASAP into stages; within a stage they are
-independent, so the engine runs them on separate lanes (several program instances -- proofs
--- packed per wave). Outputs are linear forms over atoms. Build tooling.
+A program is a straight-line formula over Fq2 values -- pairing 0.14.2's line doubling /
+addition steps with the `ell` scaling by (px, py), and the f-chain step "sparse line
+product then squaring" -- run symbolically: every Fq2 multiplication becomes a *product*
+whose operands are linear forms (Gaussian-integer coefficients c0 + c1 u) over earlier atoms
+(program inputs or products). The engine runs one program for 64 proofs at once (lane =
+proof) on NW waves (wave = product): the generator list-schedules the products into rounds
+of at most NW independent products, allocates LDS slots with reuse (a slot is rewritten
+only in a round after its last read), and emits each product's operand evaluation and each
+output's form as generated C++ (a switch on a global product / output id, so the kernel has
+exactly one inlined Fq2-product site). Build tooling; self-checking.
 
     python zebra_amd/csrc/gen_prog.py > zebra_amd/csrc/zg_prog_tables.h
 """
+import random
 import sys
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+# product kinds (zg_prog.h f2_mul_kind)
+K_MUL, K_SQR, K_MULC0, K_MULC1 = 0, 1, 2, 3
 
 
 class G(dict):
@@ -35,7 +44,7 @@ class G(dict):
     def __sub__(self, o):
         return self + (-o)
 
-    def gmul(self, c):  # multiply by Gaussian integer c = (c0, c1)
+    def gmul(self, c):
         r = G()
         for k, (a, b) in self.items():
             v = (a * c[0] - b * c[1], a * c[1] + b * c[0])
@@ -51,51 +60,38 @@ class G(dict):
 
 
 class Prog:
-    def __init__(self, name, inputs):
+    def __init__(self, name, inputs, keep=()):
         self.name = name
         self.inputs = list(inputs)
-        self.prods = []  # (L, R, stage)
-        self.stage_of = {("in", i): 0 for i in range(len(inputs))}
+        self.keep = set(keep)  # inputs whose slots must survive the program
+        self.prods = []        # (L, R, kind)
 
     def inp(self, i):
         return G({("in", i): (1, 0)})
 
+    def _p(self, x, y, kind):
+        self.prods.append((x, y, kind))
+        return G({("p", len(self.prods) - 1): (1, 0)})
+
     def mul(self, x, y):
-        st = 1 + max([self.stage_of[k] for k in list(x) + list(y)] or [0])
-        k = ("p", len(self.prods))
-        self.prods.append((x, y, st))
-        self.stage_of[k] = st
-        return G({k: (1, 0)})
+        return self._p(x, y, K_MUL)
 
     def sqr(self, x):
-        return self.mul(x, x)
+        return self._p(x, x, K_SQR)
 
-    def finish(self, outputs):
-        # renumber products grouped by stage (stable), atoms: inputs 0.., products nin..
-        order = sorted(range(len(self.prods)), key=lambda i: (self.prods[i][2], i))
-        newidx = {("p", old): len(self.inputs) + new for new, old in enumerate(order)}
-        aidx = {("in", i): i for i in range(len(self.inputs))}
-        aidx.update(newidx)
+    def mul_c0(self, x, y):  # x * y.c0 (y an input atom holding an Fq in c0)
+        return self._p(x, y, K_MULC0)
 
-        def conv(f):
-            return [(aidx[k], c0, c1) for k, (c0, c1) in sorted(f.items(), key=lambda kv: aidx[kv[0]])]
-        prods = [(conv(self.prods[o][0]), conv(self.prods[o][1]), self.prods[o][2]) for o in order]
-        nst = max(p[2] for p in prods)
-        bounds = []
-        for s in range(1, nst + 1):
-            idx = [i for i, p in enumerate(prods) if p[2] == s]
-            bounds.append((idx[0], idx[-1] + 1))
-        return {"name": self.name, "nin": len(self.inputs), "prods": prods, "stages": bounds,
-                "outs": [conv(f) for f in outputs]}
+    def mul_c1(self, x, y):  # x * y.c1
+        return self._p(x, y, K_MULC1)
 
 
 # ---------------------------------------------------------------- programs
 def prog_dbl():
-    """pairing doubling_step + ell scaling. in: X Y Z QX QY PX PY (PX = (px, 0); Q unused, the
-    layout is shared with `add`). out: X' Y' Z' A B C, the line f * (A + B v + C v w) with
-    A = c2, B = c1 px, C = c0 py"""
-    p = Prog("dbl", ["X", "Y", "Z", "QX", "QY", "PX", "PY"])
-    X, Y, Z, PX, PY = p.inp(0), p.inp(1), p.inp(2), p.inp(5), p.inp(6)
+    """pairing doubling_step + ell scaling. in: X Y Z PQ (PQ = (px, py)). out: X' Y' Z' and
+    the scaled line A + B v + C v w with A = c2, B = c1 px, C = c0 py"""
+    p = Prog("dbl", ["X", "Y", "Z", "PQ"], keep=[3])
+    X, Y, Z, PQ = (p.inp(i) for i in range(4))
     tmp0 = p.sqr(X)
     tmp1 = p.sqr(Y)
     tmp2 = p.sqr(tmp1)
@@ -112,15 +108,15 @@ def prog_dbl():
     tmp0b = p.mul(nz, zsq).dbl()
     # coeffs (c0, c1, c2) = (tmp0b, tmp3b, tmp6)
     A = tmp6
-    B = p.mul(tmp3b, PX)
-    C = p.mul(tmp0b, PY)
-    return p.finish([nx, ny, nz, A, B, C])
+    B = p.mul_c0(tmp3b, PQ)
+    C = p.mul_c1(tmp0b, PQ)
+    return p, [nx, ny, nz, A, B, C]
 
 
 def prog_add():
-    """pairing addition_step + ell scaling. in: X Y Z QX QY PX PY."""
-    p = Prog("add", ["X", "Y", "Z", "QX", "QY", "PX", "PY"])
-    X, Y, Z, QX, QY, PX, PY = (p.inp(i) for i in range(7))
+    """pairing addition_step + ell scaling. in: X Y Z PQ QX QY."""
+    p = Prog("add", ["X", "Y", "Z", "PQ", "QX", "QY"], keep=[3])
+    X, Y, Z, PQ, QX, QY = (p.inp(i) for i in range(6))
     zsq = p.sqr(Z)
     ysq = p.sqr(QY)
     t0 = p.mul(zsq, QX)
@@ -144,9 +140,9 @@ def prog_add():
     t1b = (-t6).dbl()
     # coeffs (c0, c1, c2) = (t10b, t1b, t9)
     A = t9
-    B = p.mul(t1b, PX)
-    C = p.mul(t10b, PY)
-    return p.finish([nx, ny, nz, A, B, C])
+    B = p.mul_c0(t1b, PQ)
+    C = p.mul_c1(t10b, PQ)
+    return p, [nx, ny, nz, A, B, C]
 
 
 def f6_mul_by_01(p, a, b0, b1):
@@ -155,25 +151,22 @@ def f6_mul_by_01(p, a, b0, b1):
     c0 = p.mul(a[1] + a[2], b1).nr() + t0 - t1.nr()
     c1 = p.mul(a[0] + a[1], b0 + b1) - t0 - t1
     c2 = p.mul(a[0] + a[2], b0) - t0 + t1
-    return (c0, c1, c2)
+    return [c0, c1, c2]
 
 
 def f6_mul_by_1(p, a, b1):
-    return (p.mul(a[2], b1).nr(), p.mul(a[0], b1), p.mul(a[1], b1))
+    return [p.mul(a[2], b1).nr(), p.mul(a[0], b1), p.mul(a[1], b1)]
 
 
-def prog_m014():
-    """f * (A + B v + C v w). in: f0..f5 (c0.c0 c0.c1 c0.c2 c1.c0 c1.c1 c1.c2), A, B, C."""
-    p = Prog("m014", ["F0", "F1", "F2", "F3", "F4", "F5", "A", "B", "C"])
-    f = [p.inp(i) for i in range(6)]
-    A, B, C = p.inp(6), p.inp(7), p.inp(8)
+def m014(p, f, A, B, C):
+    """f * (A + B v + C v w)   (pairing mul_by_014(c0 = A, c1 = B, c4 = C))"""
     F0, F1 = f[0:3], f[3:6]
     aa = f6_mul_by_01(p, F0, A, B)
     bb = f6_mul_by_1(p, F1, C)
     s = f6_mul_by_01(p, [x + y for x, y in zip(F0, F1)], A, B + C)
     c0 = [aa[0] + bb[2].nr(), aa[1] + bb[0], aa[2] + bb[1]]
     c1 = [s[i] - aa[i] - bb[i] for i in range(3)]
-    return p.finish(c0 + c1)
+    return c0 + c1
 
 
 def f6_mul(p, a, b):
@@ -188,82 +181,252 @@ def f6_nr(a):
     return [a[2].nr(), a[0], a[1]]
 
 
-def prog_sqr():
-    """complex squaring of an Fq12: 2 Fq6 products = 12 Fq2 products."""
-    p = Prog("sqr", ["F0", "F1", "F2", "F3", "F4", "F5"])
-    f = [p.inp(i) for i in range(6)]
+def f12_sqr(p, f):
+    """pairing Fq12::square (complex squaring: 2 Fq6 products)"""
     a0, a1 = f[0:3], f[3:6]
     ab = f6_mul(p, a0, a1)
     t = f6_mul(p, [x + y for x, y in zip(a0, a1)], [x + y for x, y in zip(a0, f6_nr(a1))])
     c0 = [t[i] - ab[i] - f6_nr(ab)[i] for i in range(3)]
     c1 = [ab[i].dbl() for i in range(3)]
-    return p.finish(c0 + c1)
+    return c0 + c1
 
 
-def prog_mul():
-    p = Prog("mul", ["A0", "A1", "A2", "A3", "A4", "A5", "B0", "B1", "B2", "B3", "B4", "B5"])
-    a = [p.inp(i) for i in range(6)]
-    b = [p.inp(6 + i) for i in range(6)]
-    t0 = f6_mul(p, a[0:3], b[0:3])
-    t1 = f6_mul(p, a[3:6], b[3:6])
-    t2 = f6_mul(p, [x + y for x, y in zip(a[0:3], a[3:6])], [x + y for x, y in zip(b[0:3], b[3:6])])
-    c0 = [t0[i] + f6_nr(t1)[i] for i in range(3)]
-    c1 = [t2[i] - t0[i] - t1[i] for i in range(3)]
-    return p.finish(c0 + c1)
+def prog_msq():
+    """f-chain step: f = (f * line)^2. in: F0..F5 A B C."""
+    p = Prog("msq", ["F0", "F1", "F2", "F3", "F4", "F5", "A", "B", "C"])
+    ins = [p.inp(i) for i in range(9)]
+    return p, f12_sqr(p, m014(p, ins[0:6], ins[6], ins[7], ins[8]))
 
 
-PROGS = [prog_dbl, prog_add, prog_m014, prog_sqr, prog_mul]
+def prog_m():
+    """f-chain step without the squaring: f = f * line. in: F0..F5 A B C."""
+    p = Prog("m", ["F0", "F1", "F2", "F3", "F4", "F5", "A", "B", "C"])
+    ins = [p.inp(i) for i in range(9)]
+    return p, m014(p, ins[0:6], ins[6], ins[7], ins[8])
 
 
-def emit(progs):
-    out = ["// GENERATED by zebra_amd/csrc/gen_prog.py -- do not edit.", "#pragma once", "#include <stdint.h>",
-           "namespace zg {", "struct PTerm { uint8_t atom; int8_t c0, c1; };  // coefficient c0 + c1 u"]
-    terms = []     # flat term pool
-    forms = []     # (offset, count)
+# ---------------------------------------------------------------- scheduling + slots
+def schedule(prog, outs, nw):
+    """list-schedule products into rounds of <= nw; allocate LDS slots with reuse."""
+    n = len(prog.prods)
+    deps = []
+    for L, R, _ in prog.prods:
+        deps.append(sorted({k[1] for k in list(L) + list(R) if k[0] == "p"}))
+    succ = [[] for _ in range(n)]
+    for i, d in enumerate(deps):
+        for j in d:
+            succ[j].append(i)
+    height = [0] * n
+    for i in reversed(range(n)):
+        height[i] = 1 + max([height[j] for j in succ[i]] or [0])
+    rnd = [None] * n
+    rounds = []
+    done = set()
+    while len(done) < n:
+        ready = [i for i in range(n) if rnd[i] is None and all(j in done for j in deps[i])]
+        ready.sort(key=lambda i: (-height[i], i))
+        pick = ready[:nw]
+        for i in pick:
+            rnd[i] = len(rounds)
+        rounds.append(pick)
+        done.update(pick)
+    nr = len(rounds)
+    # last read round of every atom (output forms are read in round nr)
+    last = {}
+    for i, (L, R, _) in enumerate(prog.prods):
+        for k in list(L) + list(R):
+            last[k] = max(last.get(k, -1), rnd[i])
+    for f in outs:
+        for k in f:
+            last[k] = max(last.get(k, -1), nr)
+    nin = len(prog.inputs)
+    slot = {("in", i): i for i in range(nin)}
+    free_at = {}  # slot -> first round it may be rewritten
+    for i in range(nin):
+        if i not in prog.keep:
+            free_at[i] = last.get(("in", i), -1) + 1
+    nslots = nin
+    for r, pick in enumerate(rounds):
+        for i in pick:
+            cand = sorted(s for s, fr in free_at.items() if fr <= r)
+            if cand:
+                s = cand[0]
+            else:
+                s = nslots
+                nslots += 1
+            slot[("p", i)] = s
+            free_at[s] = last.get(("p", i), nr) + 1
+    # outputs are written to input slots 0.. after the output round: they must not clobber a
+    # kept input
+    assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add")
+    return {"rounds": rounds, "slot": slot, "nslots": nslots, "rnd": rnd}
 
-    def add_form(f):
-        off = len(terms)
-        terms.extend(f)
-        forms.append((off, len(f)))
-        return len(forms) - 1
-    specs = []
-    for pr in progs:
-        pl = [add_form(l) for l, _, _ in pr["prods"]]
-        prr = [add_form(r) for _, r, _ in pr["prods"]]
-        po = [add_form(o) for o in pr["outs"]]
-        specs.append((pr, pl, prr, po))
-    out.append("__device__ __constant__ const PTerm PROG_TERMS[%d] = {%s};" % (
-        len(terms), ", ".join("{%d, %d, %d}" % t for t in terms)))
-    out.append("__device__ __constant__ const uint16_t PROG_FORMS[%d][2] = {%s};" % (
-        len(forms), ", ".join("{%d, %d}" % f for f in forms)))
-    out.append("struct ProgDesc { uint8_t nin, nprod, nstage, nout; uint8_t stage[8][2]; uint16_t L, R, O; };")
-    out.append("// L/R: first form index of product operands; O: first form index of outputs")
-    descs = []
-    for pr, pl, prr, po in specs:
-        st = pr["stages"] + [(0, 0)] * (8 - len(pr["stages"]))
-        assert len(pr["stages"]) <= 8
-        descs.append("{%d, %d, %d, %d, {%s}, %d, %d, %d}" % (
-            pr["nin"], len(pr["prods"]), len(pr["stages"]), len(pr["outs"]),
-            ", ".join("{%d, %d}" % s for s in st), pl[0], prr[0], po[0]))
-        out.append("#define ZG_PROG_%s %d   // %d products in %d stages, atoms %d" % (
-            pr["name"].upper(), len(descs) - 1, len(pr["prods"]), len(pr["stages"]),
-            pr["nin"] + len(pr["prods"])))
-    out.append("__device__ __constant__ const ProgDesc PROG_DESC[%d] = {%s};" % (len(descs), ", ".join(descs)))
-    maxatoms = max(pr["nin"] + len(pr["prods"]) for pr in progs)
-    out.append("#define ZG_PROG_MAXATOMS %d" % maxatoms)
+
+def simulate(prog, outs, sch, vals):
+    """run the schedule on an LDS model with the slot map; returns output values"""
+    lds = {}
+    for i, v in enumerate(vals):
+        lds[i] = v
+
+    def ev(f):
+        r0 = r1 = 0
+        for k, (c0, c1) in f.items():
+            x0, x1 = lds[sch["slot"][k]]
+            r0 += c0 * x0 - c1 * x1
+            r1 += c0 * x1 + c1 * x0
+        return (r0 % P, r1 % P)
+    for pick in sch["rounds"]:
+        res = []
+        for i in pick:
+            L, R, kind = prog.prods[i]
+            x, y = ev(L), ev(R)
+            if kind == K_MULC0:
+                y = (y[0], 0)
+            elif kind == K_MULC1:
+                y = (y[1], 0)
+            res.append((i, ((x[0] * y[0] - x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)))
+        for i, v in res:  # all reads of a round precede its writes
+            lds[sch["slot"][("p", i)]] = v
+    return [ev(f) for f in outs]
+
+
+def reference(prog, outs, vals):
+    env = {("in", i): v for i, v in enumerate(vals)}
+
+    def ev(f):
+        r0 = r1 = 0
+        for k, (c0, c1) in f.items():
+            x0, x1 = env[k]
+            r0 += c0 * x0 - c1 * x1
+            r1 += c0 * x1 + c1 * x0
+        return (r0 % P, r1 % P)
+    for i, (L, R, kind) in enumerate(prog.prods):
+        x, y = ev(L), ev(R)
+        if kind == K_MULC0:
+            y = (y[0], 0)
+        elif kind == K_MULC1:
+            y = (y[1], 0)
+        env[("p", i)] = ((x[0] * y[0] - x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)
+    return [ev(f) for f in outs]
+
+
+# ---------------------------------------------------------------- code generation
+def scaled(s, c0, c1):
+    """(C++ expression, sign) of (c0 + c1 u) * atom-in-slot-s"""
+    x = "at.get(%d)" % s
+    if (c0, c1) in ((1, 0), (-1, 0)):
+        return x, c0
+    if (c0, c1) in ((1, 1), (-1, -1)):
+        return "f2_mul_nr(%s)" % x, c0
+    if (c0, c1) in ((0, 1), (0, -1)):
+        return "f2_mul_u(%s)" % x, c1
+    if c1 == 0:
+        return "f2_smul<%d>(%s)" % (abs(c0), x), 1 if c0 > 0 else -1
+    return "f2_gmul<%d, %d>(%s)" % (c0, c1, x), 1
+
+
+def form_code(f, slot, lazy):
+    """C++ expression for a form. lazy: the value feeds a product as its lazy operand, so a
+    plain sum / difference of two canonical atoms may skip the reduction (< 2p)."""
+    terms = [scaled(slot[k], c0, c1) for k, (c0, c1) in sorted(f.items(), key=lambda kv: slot[kv[0]])]
+    terms.sort(key=lambda t: -t[1])  # a positive term first
+    if lazy and len(terms) == 2 and all(t[0].startswith("at.get") for t in terms) and terms[0][1] > 0:
+        return "f2_lz_%s(%s, %s)" % ("add" if terms[1][1] > 0 else "sub", terms[0][0], terms[1][0])
+    e, sg = terms[0]
+    acc = e if sg > 0 else "f2_neg(%s)" % e
+    for e, sg in terms[1:]:
+        acc = "f2_%s(%s, %s)" % ("add" if sg > 0 else "sub", acc, e)
+    return acc
+
+
+def emit(specs):
+    out = ["// GENERATED by zebra_amd/csrc/gen_prog.py -- do not edit.", "#pragma once",
+           "// included by zg_prog.h (needs AtomSpace and the Fq2 helpers)", "namespace zg {"]
+    prod_cases, out_cases = [], []
+    infos, sched = [], []
+    gk, go = 0, 0
+    for name, prog, outs, nw, sch in specs:
+        nin = len(prog.inputs)
+        # products
+        for i, (L, R, kind) in enumerate(prog.prods):
+            s = sch["slot"]
+            if kind == K_SQR:
+                x, y = form_code(L, s, False), "x"
+            elif kind in (K_MULC0, K_MULC1):
+                x, y = form_code(L, s, True), form_code(R, s, False)
+            else:
+                # at most one lazy operand: the one that is a plain two-term sum
+                lx = form_code(L, s, True)
+                if lx.startswith("f2_lz_"):
+                    x, y = lx, form_code(R, s, False)
+                else:
+                    x, y = form_code(R, s, True), form_code(L, s, False)
+            prod_cases.append("  case %d: x = %s; y = %s; dst = %d; return %d;  // %s p%d round %d" % (
+                gk + i, x, y, s[("p", i)], kind, name, i, sch["rnd"][i]))
+        for j, f in enumerate(outs):
+            out_cases.append("  case %d: return %s;  // %s out %d" % (go + j, form_code(f, sch["slot"], False),
+                                                                    name, j))
+        off = len(sched)
+        for pick in sch["rounds"]:
+            sched.extend(pick + [-1] * (nw - len(pick)))
+        infos.append((name, nin, len(prog.prods), len(outs), len(sch["rounds"]), nw, off, gk, go, sch["nslots"]))
+        gk += len(prog.prods)
+        go += len(outs)
+    out.append("struct ProgInfo { int nin, nprod, nout, nrounds, nw, sched, gk, go, nslots; };")
+    for k, (name, nin, npr, nout, nr, nw, off, g1, g2, ns) in enumerate(infos):
+        out.append("#define ZG_PROG_%s %d  // %d products in %d rounds of %d waves, %d LDS slots" % (
+            name.upper(), k, npr, nr, nw, ns))
+    out.append("__device__ __constant__ const ProgInfo PROG_INFO[%d] = {%s};" % (len(infos), ", ".join(
+        "{%d, %d, %d, %d, %d, %d, %d, %d, %d}" % i[1:] for i in infos)))
+    out.append("__device__ __constant__ const int8_t PROG_SCHED[%d] = {%s};" % (len(sched), ", ".join(
+        map(str, sched))))
+    for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m")))):
+        out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
+    out.append("// operands of global product gk; returns the product kind (f2_mul_kind)")
+    out.append("__device__ __forceinline__ int prog_operands(int gk, const AtomSpace& at, Fq2& x, Fq2& y, int& dst) {")
+    out.append("  switch (gk) {")
+    out.extend(prod_cases)
+    out.append("  default: x = y = f2_zero(); dst = 0; return 0;")
+    out.append("  }")
+    out.append("}")
+    out.append("__device__ __forceinline__ Fq2 prog_output(int go, const AtomSpace& at) {")
+    out.append("  switch (go) {")
+    out.extend(out_cases)
+    out.append("  default: return f2_zero();")
+    out.append("  }")
+    out.append("}")
     out.append("}  // namespace zg")
     return out
 
 
+NW_LINES = 6
+NW_FCHAIN = 8
+
+
 def build_all():
-    return [f() for f in PROGS]
+    specs = []
+    for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN)):
+        prog, outs = fn()
+        sch = schedule(prog, outs, nw)
+        specs.append((prog.name, prog, outs, nw, sch))
+    return specs
+
+
+def selfcheck(specs):
+    rng = random.Random(11)
+    for name, prog, outs, nw, sch in specs:
+        for _ in range(3):
+            vals = [(rng.randrange(P), rng.randrange(P)) for _ in prog.inputs]
+            if name in ("dbl", "add"):
+                vals[3] = (rng.randrange(P), rng.randrange(P))
+            assert simulate(prog, outs, sch, vals) == reference(prog, outs, vals), name
 
 
 if __name__ == "__main__":
-    progs = build_all()
-    for pr in progs:
-        sys.stderr.write("%s: %d products, stages %s, max |coef| %d\n" % (
-            pr["name"], len(pr["prods"]), [b - a for a, b in pr["stages"]],
-            max(max(abs(c0), abs(c1)) for f in [x for p_ in pr["prods"] for x in p_[:2]] + pr["outs"]
-                for _, c0, c1 in f)))
-    sys.stdout.write("\n".join(emit(progs)) + "\n")
+    specs = build_all()
+    selfcheck(specs)
+    for name, prog, outs, nw, sch in specs:
+        sys.stderr.write("%s: %d products, rounds %s (nw %d), %d slots\n" % (
+            name, len(prog.prods), [len(r) for r in sch["rounds"]], nw, sch["nslots"]))
+    sys.stdout.write("\n".join(emit(specs)) + "\n")

@@ -43,7 +43,6 @@ struct zg_ctx {
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
-  uint4* d_atoms = nullptr; // staged-program workspace: (cap / 64) blocks x ZG_LINES_ATOMS atoms
   G1J* d_ctree = nullptr;
   Fr* d_stree = nullptr;
   // node checks
@@ -107,7 +106,6 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
        dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
        dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3) == hipSuccess &&
-       dalloc(&ctx->d_atoms, (size_t)((cap + 63) / 64) * ZG_LINES_ATOMS * ZG_ATOM_ROWS * 64) == hipSuccess &&
        dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
        dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC) == hipSuccess;
   ok = ok && dalloc(&ctx->d_nodes, ZG_NODE_CHUNK) == hipSuccess &&
@@ -128,7 +126,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   hipSetDevice(ctx->device);
   void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
-                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines, ctx->d_atoms};
+                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -403,11 +401,9 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->side));
   // main stream: per-proof Miller loops as the R-chain (lines) + f-chain programs
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
-  hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines,
-                     ctx->d_atoms);
+  hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_batch_fchain, dim3(groups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines,
-                     ctx->d_atoms);
+  hipLaunchKernelGGL(k_batch_fchain, dim3(groups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {

@@ -93,12 +93,11 @@ __global__ void __launch_bounds__(64) k_batch_miller(BatchBufs b) {
 // Per-proof Miller loop as two staged programs (zg_prog.h; lane = proof, wave = product):
 //   k_batch_lines : the R-chain (pairing's G2Prepared steps for B_i, with the ell scaling
 //                   by r_i A_i folded in) -> 68 line triples per proof in HBM
-//   k_batch_fchain: the f-chain (sparse line products + squarings) -> ftree leaves
-// A block = 64 proofs; NW waves share each stage's independent Fq2 products.
-#define ZG_LINES_NW 6      // widest stage of dbl/add
-#define ZG_LINES_ATOMS 24  // X Y Z QX QY PX PY + up to 17 products
-#define ZG_FC_NW 12        // 3 waves per SIMD (168 VGPRs); m014 has 13 products -> 2 rounds
-#define ZG_FC_ATOMS 22     // f0..f5 A B C + up to 13 products
+//   k_batch_fchain: the f-chain (sparse line product, then squaring, fused per step)
+//                   -> ftree leaves
+// A block = 64 proofs; NW waves share each round's independent Fq2 products.
+#define ZG_LINES_NW 6   // widest round of dbl/add
+#define ZG_FC_NW 8      // 2 waves per SIMD (256 VGPRs, no spills); msq = 4 rounds
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
@@ -106,8 +105,9 @@ __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
 }
 
 // lines layout: [step][proof][A, B, C]
-__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines, uint4* wsbuf) {
-  __shared__ uint4 lds_atoms[ZG_LINES_ATOMS * ZG_ATOM_ROWS * 64];  // 144 KB
+// LDS slots (both programs): 0 X, 1 Y, 2 Z, 3 PQ = (px, py) (kept), add: 4 QX, 5 QY
+__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines) {
+  __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
   const AtomSpace at{lds_atoms};
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const int proof = blockIdx.x * 64 + lane;
@@ -125,10 +125,7 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
     at.put(0, q.x);
     at.put(1, q.y);
     at.put(2, f2_one());
-    at.put(3, q.x);
-    at.put(4, q.y);
-    at.put(5, {p.x, fp_zero<FqM>()});
-    at.put(6, {p.y, fp_zero<FqM>()});
+    at.put(3, {p.x, p.y});
   }
   __syncthreads();
   int n = 0;
@@ -136,12 +133,20 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
     for (int pass = 0; pass < 2; pass++) {
       if (pass == 1 && (i < 0 || !((ZG_XH >> i) & 1ull))) break;
       const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
-      prog_run_stages(pid, at, ZG_LINES_NW);
-      const Fq2 v = prog_out(pid, at, wave);
+      if (pid == ZG_PROG_ADD) {
+        if (wave < 2) {
+          const G2A q = b.ptB[act ? proof : 0];
+          at.put(4 + wave, wave == 0 ? (act ? q.x : f2_one()) : (act ? q.y : f2_one()));
+        }
+        __syncthreads();
+      }
+      prog_run(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
       __syncthreads();
       if (wave < 3)
         at.put(wave, v);
-      else if (proof < b.npad)
+      else if (wave < 6 && proof < b.npad)
         lines[((size_t)n * b.npad + proof) * 3 + (wave - 3)] = act ? v : f2_one();
       __syncthreads();
       n++;
@@ -149,48 +154,42 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
   }
 }
 
-__device__ __forceinline__ void fchain_step(const BatchBufs& b, const AtomSpace& at, const Fq2* lines, int n, int pid) {
-  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
-  const int proof = blockIdx.x * 64 + lane;
-  if (pid == ZG_PROG_M014) {
-    if (wave < 3) at.put(6 + wave, proof < b.npad ? lines[((size_t)n * b.npad + proof) * 3 + wave] : f2_one());
-    __syncthreads();
-  }
-  prog_run_stages(pid, at, ZG_FC_NW);
-  Fq2 v;
-  if (wave < 6) v = prog_out(pid, at, wave);
-  __syncthreads();
-  if (wave < 6) at.put(wave, v);
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines, uint4* wsbuf) {
-  __shared__ uint4 lds_atoms[ZG_FC_ATOMS * ZG_ATOM_ROWS * 64];  // 132 KB
+// LDS slots: 0..5 f (Fq2 coefficients c0.c0 c0.c1 c0.c2 c1.c0 c1.c1 c1.c2), 6..8 the line A B C
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines) {
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   const AtomSpace at{lds_atoms};
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const int proof = blockIdx.x * 64 + lane;
+  const bool inb = proof < b.npad;
+  static_assert(ZG_FC_NW >= 7, "waves 0..5 carry f, waves 6.. load the line");
   if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  for (int j = wave - 6; j >= 0 && j < 3; j += ZG_FC_NW - 6)
+    at.put(6 + j, inb ? lines[(size_t)proof * 3 + j] : f2_one());
   __syncthreads();
-  // one call site (a runtime, wave-uniform program id) keeps the engine's code single-copy:
-  // per bit i: f *= dbl line; [f *= add line]; f = f^2 -- then the last dbl line.
+  // per bit i (MSB first): [f *= dbl line; f = (f * add line)^2] or f = (f * dbl line)^2;
+  // then the last dbl line: f *= line
   int n = 0;
-  for (int i = ZG_XH_TOP, ph = 0;;) {
-    const int pid = wave_uniform(ph == 2 ? ZG_PROG_SQR : ZG_PROG_M014);
-    fchain_step(b, at, lines, n, pid);
-    if (i < 0) break;
-    if (ph == 0) {
-      ph = ((ZG_XH >> i) & 1ull) ? 1 : 2;
+  for (int i = ZG_XH_TOP;; i--) {
+    const bool last = i < 0;
+    const bool addbit = !last && ((ZG_XH >> i) & 1ull);
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
+      prog_run(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      __syncthreads();
       n++;
-    } else if (ph == 1) {
-      ph = 2;
-      n++;
-    } else {
-      ph = 0;
-      i--;
+      if (wave < 6)
+        at.put(wave, v);
+      else if (n < ZG_NCOEFF)
+        for (int j = wave - 6; j < 3; j += ZG_FC_NW - 6)
+          at.put(6 + j, inb ? lines[((size_t)n * b.npad + proof) * 3 + j] : f2_one());
+      __syncthreads();
     }
+    if (last) break;
   }
   // conjugate (u < 0) and store the leaf; inactive / padding proofs contribute 1
-  if (wave < 6 && proof < b.npad) {
+  if (wave < 6 && inb) {
     Fq2 v = at.get(wave);
     if (wave >= 3) v = f2_neg(v);
     if (!proof_active(b, proof)) v = wave == 0 ? f2_one() : f2_zero();
