@@ -86,6 +86,14 @@ ZG_INL bool fp_eq(const Fp<M>& a, const Fp<M>& b) {
 // r = a - p if a >= p else a   (a < 2p)
 template <class M>
 ZG_INL Fp<M> fp_reduce_once(const Fp<M>& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m[M::N];
+#pragma unroll
+  for (int i = 0; i < M::N; i++) m[i] = M::p(i);
+  Fp<M> r;
+  mp_reduce_once<M::N>(r.l, a.l, m);
+  return r;
+#else
   Fp<M> d;
   uint32_t borrow = 0;
 #pragma unroll
@@ -98,10 +106,19 @@ ZG_INL Fp<M> fp_reduce_once(const Fp<M>& a) {
 #pragma unroll
   for (int i = 0; i < M::N; i++) r.l[i] = borrow ? a.l[i] : d.l[i];
   return r;
+#endif
 }
 
 template <class M>
 ZG_INL Fp<M> fp_add(const Fp<M>& a, const Fp<M>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m[M::N];
+#pragma unroll
+  for (int i = 0; i < M::N; i++) m[i] = M::p(i);
+  Fp<M> r;
+  mp_add_mod<M::N>(r.l, a.l, b.l, m);
+  return r;
+#else
   Fp<M> s;
   uint32_t c = 0;
 #pragma unroll
@@ -111,10 +128,19 @@ ZG_INL Fp<M> fp_add(const Fp<M>& a, const Fp<M>& b) {
     c = (uint32_t)(t >> 32);
   }
   return fp_reduce_once<M>(s);
+#endif
 }
 
 template <class M>
 ZG_INL Fp<M> fp_sub(const Fp<M>& a, const Fp<M>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t m[M::N];
+#pragma unroll
+  for (int i = 0; i < M::N; i++) m[i] = M::p(i);
+  Fp<M> r;
+  mp_sub_mod<M::N>(r.l, a.l, b.l, m);
+  return r;
+#else
   Fp<M> d;
   uint32_t borrow = 0;
 #pragma unroll
@@ -133,6 +159,7 @@ ZG_INL Fp<M> fp_sub(const Fp<M>& a, const Fp<M>& b) {
     c = (uint32_t)(t >> 32);
   }
   return d;
+#endif
 }
 
 template <class M>
