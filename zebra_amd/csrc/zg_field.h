@@ -116,7 +116,10 @@ ZG_INL Fp<M> fp_add(const Fp<M>& a, const Fp<M>& b) {
 #pragma unroll
   for (int i = 0; i < M::N; i++) m[i] = M::p(i);
   Fp<M> r;
-  mp_add_mod<M::N>(r.l, a.l, b.l, m);
+  if constexpr (M::N == 12)
+    fqa_add(r.l, a.l, b.l);
+  else
+    mp_add_mod<M::N>(r.l, a.l, b.l, m);
   return r;
 #else
   Fp<M> s;
@@ -138,7 +141,10 @@ ZG_INL Fp<M> fp_sub(const Fp<M>& a, const Fp<M>& b) {
 #pragma unroll
   for (int i = 0; i < M::N; i++) m[i] = M::p(i);
   Fp<M> r;
-  mp_sub_mod<M::N>(r.l, a.l, b.l, m);
+  if constexpr (M::N == 12)
+    fqa_sub(r.l, a.l, b.l);
+  else
+    mp_sub_mod<M::N>(r.l, a.l, b.l, m);
   return r;
 #else
   Fp<M> d;

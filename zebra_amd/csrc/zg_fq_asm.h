@@ -33,46 +33,6 @@ __device__ __forceinline__ uint32_t shift3(Acc3& a) {
   return lo;
 }
 
-// r = a * b * 2^-384 mod p ; a, b < p  ->  r < p
-__device__ __forceinline__ void fq_mul_fips(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  constexpr int N = 12;
-  uint32_t m[N];
-  Acc3 acc = {0, 0};
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-#pragma unroll
-    for (int j = 0; j < i; j++) {
-      mac3(acc, a[j], b[i - j]);
-      mac3s(acc, m[j], FQ_P[i - j]);
-    }
-    mac3(acc, a[i], b[0]);
-    m[i] = (uint32_t)acc.lm * FQ_INV;
-    mac3s(acc, m[i], FQ_P[0]);
-    shift3(acc);
-  }
-  uint32_t t[N];
-#pragma unroll
-  for (int i = N; i < 2 * N - 1; i++) {
-#pragma unroll
-    for (int j = i - N + 1; j < N; j++) {
-      mac3(acc, a[j], b[i - j]);
-      mac3s(acc, m[j], FQ_P[i - j]);
-    }
-    t[i - N] = shift3(acc);
-  }
-  t[N - 1] = (uint32_t)acc.lm;  // < 2p < 2^382: no further carry
-  // conditional subtraction
-  uint32_t d[N], borrow = 0;
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    uint64_t s = (uint64_t)t[i] - FQ_P[i] - borrow;
-    d[i] = (uint32_t)s;
-    borrow = (uint32_t)(s >> 63);
-  }
-#pragma unroll
-  for (int i = 0; i < N; i++) r[i] = borrow ? t[i] : d[i];
-}
-
 // ---- multi-limb add / sub / select on VALU carry chains (device only).
 // The C formulation (uint64_t sums, >> 32 carries) compiles to 64-bit shift-adds and moves,
 // ~5 instructions per limb; these are 1 (v_add_co / v_addc_co / v_sub_co / v_subb_co with
@@ -146,5 +106,7 @@ __device__ __forceinline__ void mp_sub_mod(uint32_t* r, const uint32_t* a, const
 #pragma unroll
   for (int i = 0; i < N; i++) r[i] = asm_sel(d[i], e[i], bo);  // borrow: a < b, add m back
 }
+
+#include "zg_fips.h"
 
 }  // namespace zg

@@ -24,10 +24,27 @@ struct Fq12 {
 ZG_INL Fq2 f2_zero() { return {fp_zero<FqM>(), fp_zero<FqM>()}; }
 ZG_INL Fq2 f2_one() { return {fq_one(), fp_zero<FqM>()}; }
 ZG_INL Fq2 f2_const(const uint32_t c[2][12]) { return {fq_const(c[0]), fq_const(c[1])}; }
-ZG_INL Fq2 f2_add(const Fq2& a, const Fq2& b) { return {fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)}; }
-ZG_INL Fq2 f2_sub(const Fq2& a, const Fq2& b) { return {fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)}; }
-ZG_INL Fq2 f2_neg(const Fq2& a) { return {fq_neg(a.c0), fq_neg(a.c1)}; }
-ZG_INL Fq2 f2_dbl(const Fq2& a) { return {fq_dbl(a.c0), fq_dbl(a.c1)}; }
+// device: both coefficients' carry chains in one interleaved asm statement (zg_fips.h)
+ZG_INL Fq2 f2_add(const Fq2& a, const Fq2& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  Fq2 r;
+  f2a_add(r.c0.l, a.c0.l, b.c0.l, r.c1.l, a.c1.l, b.c1.l);
+  return r;
+#else
+  return {fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)};
+#endif
+}
+ZG_INL Fq2 f2_sub(const Fq2& a, const Fq2& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  Fq2 r;
+  f2a_sub(r.c0.l, a.c0.l, b.c0.l, r.c1.l, a.c1.l, b.c1.l);
+  return r;
+#else
+  return {fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)};
+#endif
+}
+ZG_INL Fq2 f2_neg(const Fq2& a) { return f2_sub({fp_zero<FqM>(), fp_zero<FqM>()}, a); }
+ZG_INL Fq2 f2_dbl(const Fq2& a) { return f2_add(a, a); }
 ZG_INL Fq2 f2_conj(const Fq2& a) { return {a.c0, fq_neg(a.c1)}; }
 ZG_INL bool f2_is_zero(const Fq2& a) { return fq_is_zero(a.c0) && fq_is_zero(a.c1); }
 ZG_INL bool f2_eq(const Fq2& a, const Fq2& b) { return fq_eq(a.c0, b.c0) && fq_eq(a.c1, b.c1); }
@@ -44,7 +61,15 @@ ZG_INL Fq2 f2_sqr(const Fq2& a) {
 }
 ZG_INL Fq2 f2_mul_fq(const Fq2& a, const Fq& s) { return {fq_mul(a.c0, s), fq_mul(a.c1, s)}; }
 // multiply by xi = u + 1
-ZG_INL Fq2 f2_mul_nr(const Fq2& a) { return {fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1)}; }
+ZG_INL Fq2 f2_mul_nr(const Fq2& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  Fq2 r;
+  f2a_sub_add(r.c0.l, a.c0.l, a.c1.l, r.c1.l, a.c0.l, a.c1.l);
+  return r;
+#else
+  return {fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1)};
+#endif
+}
 ZG_NOINL inline void f2_inv_p(Fq2* r, const Fq2* ap) {
   const Fq2 a = *ap;
   Fq t = fq_inv(fq_add(fq_sqr(a.c0), fq_sqr(a.c1)));
