@@ -61,7 +61,9 @@ extern "C" {
 #define ZG_MAX_INPUTS 9
 #define ZG_INPUT_STRIDE (ZG_MAX_INPUTS * ZG_FR_BYTES) /* 288 B per proof, unused slots ignored */
 #define ZG_GT_BYTES 576 /* Fq12: 12 x 48-byte big-endian canonical coefficients, tower order */
-#define ZG_R_BYTES 16   /* batch scalar r_i: 128-bit little-endian, non-zero */
+#define ZG_R_BYTES 16   /* batch scalar r_i: two little-endian u64 (a, b) meaning
+                           r_i = (2a + 1) + b * lambda mod r, lambda = -x^2 mod r (the G1
+                           endomorphism's eigenvalue): 2^128 distinct non-zero scalars */
 
 typedef struct zg_config {
   int device;         /* HIP device ordinal (one process per GPU) */

@@ -150,6 +150,17 @@ def batch_scalar(seed, i):
     return int.from_bytes(h, "little") or 1
 
 
+LAMBDA = (-B.BLS_X * B.BLS_X) % B.R   # sigma(x, y) = (beta x, y) acts as [LAMBDA] on G1
+
+
+def batch_r(r16):
+    """The batch scalar of the C ABI (include/zg.h ZG_R_BYTES): 16 bytes = LE u64 (a, b),
+    r = (2a + 1) + b * LAMBDA mod R -- 2^128 distinct non-zero values (GLV-friendly)."""
+    a = int.from_bytes(bytes(r16[:8]), "little")
+    b = int.from_bytes(bytes(r16[8:16]), "little")
+    return (2 * a + 1 + b * LAMBDA) % B.R
+
+
 def rerandomize(proof, delta_g2, t, s):
     """(A, B, C) -> (t^-1 A, t B + t s delta, C + s A): valid iff the source is
     (e(A',B') = e(A,B) e(sA, delta), C' = C + sA)."""

@@ -319,17 +319,19 @@ def main():
             pb = pb[144:] + pb[48:144] + pb[:48]
         elif c == "zero_proof":
             pb = bytes(192)
-        r = G.batch_scalar(seed, i)
+        r16 = G.batch_scalar(seed, i).to_bytes(16, "little")
+        r = G.batch_r(r16)
         st, gt = G.verify_status(pvks[kind], pb, inp)
         batch["items"].append({"src": e["name"], "kind": kind, "proof": hx(pb), "inputs": [fr_hex(v) for v in inp],
-                               "r": r.to_bytes(16, "little").hex(), "status": st, "corruption": c,
+                               "r": r16.hex(), "status": st, "corruption": c,
                                "lhs_gt": hx(B.f12_to_bytes(gt)) if gt is not None else None})
         if st in (G.OK, G.VERIFY_FAILED):
             lhs.append(gt)
             rs.append(r)
         print("batch", i, st, flush=True)
     batch["gt_out"] = hx(B.f12_to_bytes(G.batch_gt(lhs, rs)))
-    batch["gt_out_def"] = "prod over proofs with status OK or VERIFY_FAILED of lhs_gt^r"
+    batch["gt_out_def"] = ("prod over proofs with status OK or VERIFY_FAILED of lhs_gt^r, r = oracle.groth16.batch_r"
+                           "(16 r bytes) = (2a + 1) + b lambda")
 
     # all-valid sub-batch (first 64 without corruptions) accumulated GT
     out = {
@@ -347,5 +349,26 @@ def main():
         print("wrote", fn)
 
 
+def refresh_batch_gt():
+    """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
+    change of the batch-scalar mapping; no reference sources needed)"""
+    path = os.path.join(HERE, "batch64.json")
+    batch = json.load(open(path))
+    lhs, rs = [], []
+    for it in batch["items"]:
+        if it["status"] in (G.OK, G.VERIFY_FAILED):
+            lhs.append(B.f12_from_bytes(bytes.fromhex(it["lhs_gt"])))
+            rs.append(G.batch_r(bytes.fromhex(it["r"])))
+    batch["gt_out"] = hx(B.f12_to_bytes(G.batch_gt(lhs, rs)))
+    batch["gt_out_def"] = ("prod over proofs with status OK or VERIFY_FAILED of lhs_gt^r, r = oracle.groth16.batch_r"
+                           "(16 r bytes) = (2a + 1) + b lambda")
+    with open(path, "w") as f:
+        json.dump(batch, f, indent=1, sort_keys=True)
+    print("refreshed gt_out of batch64.json")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--refresh-batch-gt":
+        refresh_batch_gt()
+    else:
+        main()

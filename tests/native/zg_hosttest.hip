@@ -63,6 +63,21 @@ int zgt_g2_decompress(const uint8_t* b, uint8_t* out) {
   }
   return r;
 }
+// [r] P with the batch-scalar GLV path (r from 16 bytes, zg_groth16.h); affine x || y out
+void zgt_g1_glv_mul(const uint8_t* xy, const uint8_t* r16, uint8_t* out) {
+  uint64_t a, b;
+  batch_scalar_ab(r16, &a, &b);
+  G1A r = jac_to_aff(g1_glv_mul({ld_fq(xy), ld_fq(xy + 48), false}, a, b));
+  st_fq(r.x, out);
+  st_fq(r.y, out + 48);
+}
+// the batch scalar as a canonical little-endian Fr
+void zgt_batch_scalar(const uint8_t* r16, uint8_t* out) {
+  uint64_t a, b;
+  batch_scalar_ab(r16, &a, &b);
+  Fr v = fr_from_mont(batch_scalar_fr(a, b));
+  memcpy(out, v.l, 32);
+}
 int zgt_g1_in_subgroup(const uint8_t* xy) { return g1_in_subgroup({ld_fq(xy), ld_fq(xy + 48), false}); }
 int zgt_g2_in_subgroup(const uint8_t* xy) {
   return g2_in_subgroup({{ld_fq(xy), ld_fq(xy + 48)}, {ld_fq(xy + 96), ld_fq(xy + 144)}, false});

@@ -178,5 +178,5 @@ def test_partial_bitexact_vs_oracle(ctx):
     ctx.batch_finish(True, len(items))
     want = G.batch_partial(pvks, [(e["kind"], bytes.fromhex(e["proof"]),
                                    [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]],
-                                   int.from_bytes(bytes.fromhex(e["r"]), "little")) for e in items])
+                                   G.batch_r(bytes.fromhex(e["r"]))) for e in items])
     assert part == B.f12_to_bytes(want)

@@ -147,3 +147,23 @@ def test_lazy_linear_forms(L):
             got = sum(int(out[i]) << (32 * i) for i in range(12))
             assert got % P == want
             assert got < (P if canon else (22 * P) // 10)
+
+
+def test_batch_scalar_glv(L):
+    """zg_groth16.h: r_i = (2a+1) + b lambda from 16 bytes, and [r_i] P by the sign-aligned GLV
+    columns, against the oracle's plain scalar multiplication."""
+    from oracle import groth16 as G
+    rng = random.Random(9)
+    out = hostlib.buf(96)
+    fr = hostlib.buf(32)
+    assert (G.LAMBDA * G.LAMBDA + G.LAMBDA + 1) % B.R == 0
+    cases = [bytes(16), b"\xff" * 16, b"\xff" * 8 + bytes(8), bytes(8) + b"\xff" * 8]
+    cases += [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(8)]
+    for k, r16 in enumerate(cases):
+        r = G.batch_r(r16)
+        L.zgt_batch_scalar(r16, fr)
+        assert int.from_bytes(fr.raw, "little") == r
+        p = B.ec_mul(B.FQ, B.G1_GEN, 1 + 7919 * k)
+        L.zgt_g1_glv_mul(fq_b(p[0]) + fq_b(p[1]), r16, out)
+        q = B.ec_mul(B.FQ, p, r)
+        assert (int.from_bytes(out.raw[:48], "big"), int.from_bytes(out.raw[48:], "big")) == q

@@ -340,11 +340,7 @@ static void gen_scalars(zg_ctx* ctx, size_t n, std::vector<uint8_t>& r) {
       off += (size_t)got;
     }
   }
-  for (size_t i = 0; i < n; i++) {  // r_i != 0
-    uint8_t acc = 0;
-    for (int b = 0; b < 16; b++) acc |= r[16 * i + b];
-    if (!acc) r[16 * i] = 1;
-  }
+  // any 16 bytes are a valid batch scalar: r_i = (2a + 1) + b lambda != 0 (zg_groth16.h)
 }
 
 static BatchBufs batch_bufs(zg_ctx* ctx) {
@@ -385,7 +381,12 @@ static int run_pipeline(zg_ctx* ctx) {
   static const int root = 1;
   HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  hipLaunchKernelGGL(k_batch_decode, dim3(nblocks(ctx->npad)), dim3(ZG_BLOCK), 0, ctx->stream, b);
+  // one wave per 64 proofs fills every SIMD from 64k proofs up; below, split the chains
+  const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
+  if (dgroups >= 1024)
+    hipLaunchKernelGGL(k_batch_decode<1>, dim3(dgroups), dim3(64), 0, ctx->stream, b);
+  else
+    hipLaunchKernelGGL(k_batch_decode<3>, dim3(dgroups), dim3(192), 0, ctx->stream, b);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   // side stream
