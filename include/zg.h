@@ -127,6 +127,34 @@ int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
 int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
 int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);
 
+/* ---- host-side public-input preparation (CPU; no context, no GPU). The reference does this
+ * in Rust before calling bellman; these restate it so a caller can go from description bytes
+ * to the `inputs` rows of zg_verify_batch. Returns ZG_PREP_* (>= 0) or ZG_E_INVAL.
+ *   zg_prep_spend      <- accept_spend      verification/src/sapling.rs:101-155 (7 x 32 B out:
+ *                         rk.x rk.y cv.x cv.y anchor nf0 nf1; the spend_auth_sig check stays
+ *                         with the caller, between the rk check and the proof)
+ *   zg_prep_output     <- accept_output     verification/src/sapling.rs:171-200 (5 x 32 B out:
+ *                         cv.x cv.y epk.x epk.y cmu)
+ *   zg_prep_joinsplit  <- sprout::verify    verification/src/sprout.rs:34-58,86-153 (9 x 32 B)
+ *   zg_hsig            <- compute_hsig      verification/src/sprout.rs:16-32 */
+#define ZG_PREP_OK 0
+#define ZG_PREP_VALUE_COMMITMENT_INVALID 1     /* ValueCommitment(Invalid) */
+#define ZG_PREP_VALUE_COMMITMENT_SMALL_ORDER 2 /* ValueCommitment(SmallOrder) */
+#define ZG_PREP_ANCHOR 3                       /* SpendError::Anchor */
+#define ZG_PREP_RANDOMIZED_KEY_INVALID 4       /* SpendError::RandomizedKey(Invalid) */
+#define ZG_PREP_RANDOMIZED_KEY_SMALL_ORDER 5   /* SpendError::RandomizedKey(SmallOrder) */
+#define ZG_PREP_NOTE_COMMITMENT 6              /* OutputError::NoteCommitment */
+#define ZG_PREP_EPHEMERAL_KEY_INVALID 7        /* OutputError::EphemeralKey(Invalid) */
+#define ZG_PREP_EPHEMERAL_KEY_SMALL_ORDER 8    /* OutputError::EphemeralKey(SmallOrder) */
+int zg_prep_spend(const uint8_t cv[32], const uint8_t anchor[32], const uint8_t nullifier[32], const uint8_t rk[32],
+                  uint8_t inputs[7 * 32]);
+int zg_prep_output(const uint8_t cv[32], const uint8_t cmu[32], const uint8_t epk[32], uint8_t inputs[5 * 32]);
+int zg_prep_joinsplit(const uint8_t anchor[32], const uint8_t random_seed[32], const uint8_t nullifiers[64],
+                      const uint8_t macs[64], const uint8_t commitments[64], uint64_t vpub_old, uint64_t vpub_new,
+                      const uint8_t pubkey[32], uint8_t inputs[9 * 32]);
+int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32], const uint8_t pubkey[32],
+            uint8_t out[32]);
+
 /* ---- synthetic workload (bench/tests): Groth16 re-randomization of real proofs,
  * out[i] = rerandomize(src[src_index[i]]) with (t, s) = BLAKE2b-512("zg-rerand"||seed||i)
  * (A,B,C) -> (t^-1 A, t B + t s delta, C + s A); valid iff the source is. */

@@ -1,0 +1,156 @@
+"""The block-level collector (zebra_amd/collector.py) keeps the
+reference's error precedence while verifying a whole block in one batch.
+
+CPU tier: the collector's ordering logic on the reference's real transactions, with the
+oracle's C++ bellman restatement as the per-proof verifier (checker only).
+GPU tier: config 5 -- a replayed block stream mixing Sprout-Groth16 and
+Sapling proofs 1 : 4 (Groth16 re-randomization, seed 4) through the product path: all accept,
+and a single corrupted JoinSplit surfaces as InvalidJoinSplit(idx) on the right tx."""
+import random
+
+import pytest
+
+from tests.conftest import load_golden
+
+SRC_TX = {"bd4fe81c": ["S1", "O1"], "smoky": ["J1"], "991edf59": ["S2", "O3"], "56afac11": ["O2"],
+          "53cf8971": ["J2"], "a2a2fe38": ["J3"], "70abe357": ["J4"]}
+
+
+def h(x):
+    return bytes.fromhex(x)
+
+
+def fields():
+    tf = load_golden("input_prep.json")["tx_fields"]
+    out = {}
+    for kind in ("spends", "outputs", "joinsplits"):
+        for e in tf[kind]:
+            out[e["name"]] = e
+    return out
+
+
+def make_tx(names, F, proof_of=None):
+    """a transaction carrying the named real descriptions (proof bytes optionally replaced)"""
+    from zebra_amd.collector import JoinSplit, Output, Spend, Tx
+    tx = Tx()
+    for nm in names:
+        e = F[nm]
+        pb = proof_of(nm) if proof_of else h(e["zkproof"])
+        if nm[0] == "J":
+            tx.js_pubkey = h(e["pubkey"])
+            tx.joinsplits.append(JoinSplit(h(e["anchor"]), h(e["random_seed"]), [h(x) for x in e["nullifiers"]],
+                                           [h(x) for x in e["macs"]], [h(x) for x in e["commitments"]],
+                                           e["vpub_old"], e["vpub_new"], pb))
+        elif nm[0] == "S":
+            tx.spends.append(Spend(h(e["cv"]), h(e["anchor"]), h(e["nullifier"]), h(e["rk"]), pb))
+        else:
+            tx.outputs.append(Output(h(e["cv"]), h(e["cmu"]), h(e["epk"]), pb))
+    return tx
+
+
+@pytest.fixture(scope="module")
+def cpu_verify():
+    from tests import cpulib
+    L = cpulib.load()
+
+    def verify(proofs, kinds, inputs, n_inputs):
+        return cpulib.verify(L, proofs, kinds, inputs, n_inputs, threads=8)[0]
+    return verify
+
+
+def test_real_block_accepts(cpu_verify):
+    from zebra_amd.collector import verify_block
+    F = fields()
+    txs = [make_tx(v, F) for v in SRC_TX.values()]
+    assert verify_block(txs, verify=cpu_verify) is None
+
+
+def test_error_precedence(cpu_verify):
+    """lowest failing tx wins; inside a tx: JoinSplit sig -> JS proofs (index) with tree roots in
+    between -> JS nullifiers -> Sapling (any spend/output/binding failure) -> Sapling nullifiers"""
+    from zebra_amd.collector import verify_block
+    F = fields()
+    bad = bytearray(h(F["J1"]["zkproof"]))
+    bad[100] ^= 1   # corrupts B -> decode failure or verify failure: either way InvalidJoinSplit
+
+    def txs():
+        # a tx's JoinSplits share its pubkey: tx 1 carries J1 twice
+        return [make_tx(["S1", "O1"], F), make_tx(["J1", "J1"], F), make_tx(["S2", "O3"], F)]
+    t = txs()
+    t[1].joinsplits[1].zkproof = bytes(bad)
+    assert verify_block(t, verify=cpu_verify) == (1, ("InvalidJoinSplit", 1))
+    t = txs()
+    t[2].spends[0].cv = bytes(32)                    # small-order cv -> prep error -> InvalidSapling
+    assert verify_block(t, verify=cpu_verify) == (2, "InvalidSapling")
+    t[1].joinsplits[0].tree_error = "UnknownAnchor"  # lower tx index wins
+    assert verify_block(t, verify=cpu_verify) == (1, "UnknownAnchor")
+    t[1].joinsplits[0].zkproof = bytes(bad)          # JS 0 proof precedes its own tree root
+    assert verify_block(t, verify=cpu_verify) == (1, ("InvalidJoinSplit", 0))
+    t[1].js_sig_ok = False                           # ed25519 sig precedes the proofs
+    assert verify_block(t, verify=cpu_verify) == (1, "JoinSplitSignature")
+    t[0].pre_error = "Eval"                          # an earlier tx's transparent failure wins
+    assert verify_block(t, verify=cpu_verify) == (0, "Eval")
+    t = txs()
+    t[0].spends[0].sig_ok = False
+    t[0].sapling_nullifier_error = "SaplingNullifiers"
+    assert verify_block(t, verify=cpu_verify) == (0, "InvalidSapling")
+    t = txs()
+    t[0].sapling_nullifier_error = "SaplingNullifiers"
+    assert verify_block(t, verify=cpu_verify) == (0, "SaplingNullifiers")
+    t = txs()
+    t[1].js_nullifier_error = "JoinSplitNullifiers"
+    t[1].joinsplits[0].zkproof = bytes(bad)
+    assert verify_block(t, verify=cpu_verify) == (1, ("InvalidJoinSplit", 0))
+
+
+@pytest.mark.gpu
+def test_config5_replay_block_stream():
+    """config 5: blocks of re-randomized real transactions, Sprout-Groth16 : Sapling = 1 : 4 by
+    proof count, one zg_verify_batch per block; a corrupted JS surfaces on its tx and index."""
+    from zebra_amd import Context
+    from zebra_amd.collector import verify_block
+    F = fields()
+    real = {e["name"]: e for e in load_golden("real_proofs.json")["proofs"]}
+    names = ["S1", "S2", "O1", "O2", "O3", "J1", "J2", "J3", "J4"]
+    ctx = Context(device=0, max_batch=4096)
+    try:
+        src = b"".join(h(real[n]["proof"]) for n in names)
+        kinds = bytes(real[n]["kind"] for n in names)
+        rng = random.Random(4)
+        sap = [v for v in SRC_TX.values() if v[0][0] != "J"]
+        spr = [v for v in SRC_TX.values() if v[0][0] == "J"]
+        blocks = []
+        for b in range(6):
+            txs_names = []
+            nsap = nspr = 0
+            while nsap + nspr < 400:
+                if nspr * 4 < nsap:
+                    pick = rng.choice(spr)
+                    nspr += len(pick)
+                else:
+                    pick = rng.choice(sap)
+                    nsap += len(pick)
+                txs_names.append(pick)
+            blocks.append(txs_names)
+        for bi, txs_names in enumerate(blocks):
+            flat = [n for t in txs_names for n in t]
+            rr = ctx.synth_rerandomize(src, kinds, [names.index(n) for n in flat], 4000 + bi)
+            it = iter(range(len(flat)))
+            proofs = {}
+            txs = []
+            for t in txs_names:
+                cur = {}
+                for n in t:
+                    k = next(it)
+                    cur[n] = rr[192 * k:192 * k + 192]
+                txs.append(make_tx(t, F, proof_of=lambda n, cur=cur: cur[n]))
+                proofs[len(txs) - 1] = cur
+            assert verify_block(txs, ctx=ctx) is None, bi
+            if bi == 2:   # one corrupted JoinSplit proof (A <-> C swapped) in a late tx
+                js_tx = [i for i, t in enumerate(txs_names) if t[0][0] == "J"]
+                ti = js_tx[len(js_tx) // 2]
+                pb = txs[ti].joinsplits[0].zkproof
+                txs[ti].joinsplits[0].zkproof = pb[144:] + pb[48:144] + pb[:48]
+                assert verify_block(txs, ctx=ctx) == (ti, ("InvalidJoinSplit", 0))
+    finally:
+        ctx.close()

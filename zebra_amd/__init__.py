@@ -6,4 +6,4 @@ The product is the HIP library ``zebra_amd/libzg.so`` behind the C ABI ``include
 """
 from .zg import (Context, ZgError, KIND_SPEND, KIND_OUTPUT, KIND_SPROUT, KIND_NINPUTS, STATUS_OK,  # noqa: F401
                  STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL,
-                 STATUS_NAMES, pack_inputs)
+                 STATUS_NAMES, pack_inputs, prep_spend, prep_output, prep_joinsplit, hsig, PrepError)

@@ -1,0 +1,168 @@
+"""Block-level Groth16 collector -- the caller side of the boundary.
+
+Restates how the reference's chain acceptor reaches the proof checks, so that a whole block
+(or import window) is verified with ONE batch call while the reported error stays exactly the
+reference's:
+
+  ChainAcceptor::check_transactions   verification/src/accept_chain.rs:76-81
+      rayon fold/reduce over transactions: the LOWEST failing tx index wins
+  TransactionAcceptor::check          verification/src/accept_transaction.rs:68-84
+      ... -> eval (sighash) -> join_split.check -> sapling.check
+  JoinSplitVerification::check        accept_transaction.rs:649-657
+      ed25519 JoinSplit signature -> JoinSplitProof::check -> JoinSplit nullifiers
+  JoinSplitProof::check               accept_transaction.rs:575-596
+      per description i: sprout::verify (-> InvalidJoinSplit(i)), then tree_cache.continue_root
+  SaplingVerification                 accept_transaction.rs:700-714 (SaplingProof::check)
+      accept_sapling (sapling.rs:75-98): per spend (cv, anchor, rk, spend_auth_sig, proof),
+      per output (cv, cmu, epk, proof), binding signature -> any failure is InvalidSapling;
+      then Sapling nullifiers
+
+The checks that are not Groth16 (signatures, tree roots, nullifiers, the transparent
+checks before the shielded stages, PGHR13 proofs of pre-Sapling JoinSplits) are evaluated by
+the caller exactly as today and handed in as outcomes; the collector prepares every Groth16
+public input with the product's host code (zg_prep_*), verifies all proofs of the block in
+one zg_verify_batch call and re-injects the per-proof statuses in reference order.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import zg
+
+OK = zg.STATUS_OK
+
+
+@dataclass
+class JoinSplit:
+    """one JoinSplit description (chain/src/join_split.rs:169-186)"""
+    anchor: bytes
+    random_seed: bytes
+    nullifiers: List[bytes]
+    macs: List[bytes]
+    commitments: List[bytes]
+    vpub_old: int
+    vpub_new: int
+    zkproof: bytes                    # 192 B Groth16 (v4+) or 296 B PGHR13
+    groth: bool = True
+    pghr_ok: Optional[bool] = None    # caller's PGHR13 verdict for a non-Groth description
+    tree_error: Optional[str] = None  # caller's tree_cache.continue_root outcome (None = ok)
+
+
+@dataclass
+class Spend:
+    cv: bytes
+    anchor: bytes
+    nullifier: bytes
+    rk: bytes
+    zkproof: bytes
+    sig_ok: bool = True               # caller's spend_auth_sig (RedJubjub) verdict
+
+
+@dataclass
+class Output:
+    cv: bytes
+    cmu: bytes
+    epk: bytes
+    zkproof: bytes
+
+
+@dataclass
+class Tx:
+    """the shielded-proof view of one transaction, with the caller's non-Groth16 outcomes"""
+    pre_error: Optional[str] = None           # first failing check before the JoinSplit stage
+    js_pubkey: Optional[bytes] = None
+    js_sig_ok: bool = True
+    joinsplits: List[JoinSplit] = field(default_factory=list)
+    js_nullifier_error: Optional[str] = None
+    spends: List[Spend] = field(default_factory=list)
+    outputs: List[Output] = field(default_factory=list)
+    binding_ok: bool = True
+    sapling_nullifier_error: Optional[str] = None
+
+
+def _queue(txs):
+    """prepare inputs; returns (items, per-tx plans). A plan entry refers to a queued proof by
+    index, or carries a prep error."""
+    items, plans = [], []
+    for tx in txs:
+        js_plan, sp_plan, out_plan = [], [], []
+        for d in tx.joinsplits:
+            if not d.groth or tx.js_pubkey is None:
+                js_plan.append(("caller", bool(d.pghr_ok)))
+                continue
+            inp = zg.prep_joinsplit(d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old,
+                                    d.vpub_new, tx.js_pubkey)
+            js_plan.append(("proof", len(items)))
+            items.append((zg.KIND_SPROUT, bytes(d.zkproof), inp))
+        for s in tx.spends:
+            try:
+                inp = zg.prep_spend(s.cv, s.anchor, s.nullifier, s.rk)
+            except zg.PrepError as e:
+                sp_plan.append(("prep", e.name))
+                continue
+            sp_plan.append(("proof", len(items)))
+            items.append((zg.KIND_SPEND, bytes(s.zkproof), inp))
+        for o in tx.outputs:
+            try:
+                inp = zg.prep_output(o.cv, o.cmu, o.epk)
+            except zg.PrepError as e:
+                out_plan.append(("prep", e.name))
+                continue
+            out_plan.append(("proof", len(items)))
+            items.append((zg.KIND_OUTPUT, bytes(o.zkproof), inp))
+        plans.append((js_plan, sp_plan, out_plan))
+    return items, plans
+
+
+def _tx_error(tx, plan, status):
+    """the reference's first error of one transaction, given the proof statuses"""
+    js_plan, sp_plan, out_plan = plan
+    if tx.pre_error:
+        return tx.pre_error
+    if tx.joinsplits:
+        if not tx.js_sig_ok:
+            return "JoinSplitSignature"
+        for i, (d, (how, v)) in enumerate(zip(tx.joinsplits, js_plan)):
+            ok = v if how == "caller" else status[v] == OK
+            if not ok:
+                return ("InvalidJoinSplit", i)
+            if d.tree_error:
+                return d.tree_error
+        if tx.js_nullifier_error:
+            return tx.js_nullifier_error
+    if tx.spends or tx.outputs:
+        for s, (how, v) in zip(tx.spends, sp_plan):
+            if how == "prep" or not s.sig_ok or status[v] != OK:
+                return "InvalidSapling"
+        for how, v in out_plan:
+            if how == "prep" or status[v] != OK:
+                return "InvalidSapling"
+        if not tx.binding_ok:
+            return "InvalidSapling"
+        if tx.sapling_nullifier_error:
+            return tx.sapling_nullifier_error
+    return None
+
+
+def verify_block(txs, verify=None, ctx=None):
+    """Check the shielded proofs of a block (or an import window: a flat list of Tx in chain
+    order). Returns None if every transaction passes, else (tx_index, error) with the error the
+    reference reports (accept_chain.rs:79-80: the lowest failing index wins).
+
+    verify(proofs, kinds, inputs, n_inputs) -> statuses; default: ctx.verify_batch (ONE GPU
+    batch for the whole block, exact per-proof statuses via bisection)."""
+    items, plans = _queue(txs)
+    if verify is None:
+        def verify(proofs, kinds, inputs, n_inputs):
+            return ctx.verify_batch(proofs, kinds, inputs, n_inputs)[0]
+    status = []
+    if items:
+        proofs = b"".join(p for _, p, _ in items)
+        kinds = bytes(k for k, _, _ in items)
+        inputs = zg.pack_inputs([inp for _, _, inp in items])
+        n_inputs = bytes(len(inp) for _, _, inp in items)
+        status = list(verify(proofs, kinds, inputs, n_inputs))
+    for idx, (tx, plan) in enumerate(zip(txs, plans)):
+        err = _tx_error(tx, plan, status)
+        if err is not None:
+            return idx, err
+    return None

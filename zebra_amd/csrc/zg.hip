@@ -14,6 +14,7 @@
 #include "../../include/zg.h"
 #include "zg_blake2b.h"
 #include "zg_kernels.h"
+#include "zg_prep.h"
 #include "zg_vk_embed.h"  // generated from zebra_amd/res/*.json by zebra_amd/build.py
 
 using namespace zg;
@@ -627,6 +628,37 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
 extern "C" int zg_last_timings(zg_ctx* ctx, float* ms6) {
   if (!ctx || !ms6) return ZG_E_INVAL;
   for (int i = 0; i < 6; i++) ms6[i] = ctx->timings[i];
+  return ZG_OK;
+}
+
+// ------------------------------------------------------------------ host input preparation
+// (zg_prep.h). CPU only: no context, no GPU.
+extern "C" int zg_prep_spend(const uint8_t cv[32], const uint8_t anchor[32], const uint8_t nullifier[32],
+                             const uint8_t rk[32], uint8_t inputs[7 * 32]) {
+  if (!cv || !anchor || !nullifier || !rk || !inputs) return ZG_E_INVAL;
+  return prep_spend(cv, anchor, nullifier, rk, inputs);
+}
+
+extern "C" int zg_prep_output(const uint8_t cv[32], const uint8_t cmu[32], const uint8_t epk[32],
+                              uint8_t inputs[5 * 32]) {
+  if (!cv || !cmu || !epk || !inputs) return ZG_E_INVAL;
+  return prep_output(cv, cmu, epk, inputs);
+}
+
+extern "C" int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32],
+                       const uint8_t pubkey[32], uint8_t out[32]) {
+  if (!random_seed || !nf0 || !nf1 || !pubkey || !out) return ZG_E_INVAL;
+  prep_hsig(random_seed, nf0, nf1, pubkey, out);
+  return ZG_OK;
+}
+
+extern "C" int zg_prep_joinsplit(const uint8_t anchor[32], const uint8_t random_seed[32],
+                                 const uint8_t nullifiers[64], const uint8_t macs[64],
+                                 const uint8_t commitments[64], uint64_t vpub_old, uint64_t vpub_new,
+                                 const uint8_t pubkey[32], uint8_t inputs[9 * 32]) {
+  if (!anchor || !random_seed || !nullifiers || !macs || !commitments || !pubkey || !inputs) return ZG_E_INVAL;
+  prep_joinsplit(anchor, random_seed, nullifiers, nullifiers + 32, macs, macs + 32, commitments, commitments + 32,
+                 vpub_old, vpub_new, pubkey, inputs);
   return ZG_OK;
 }
 

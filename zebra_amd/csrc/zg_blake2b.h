@@ -1,6 +1,7 @@
-// zg_blake2b.h -- BLAKE2b (RFC 7693), host side, unkeyed, no salt/personalization.
-// Used only to derive batch scalars r_i in seeded mode and synthetic re-randomization
-// scalars; the product's production mode draws r_i from the OS RNG.
+// zg_blake2b.h -- BLAKE2b (RFC 7693), host side, unkeyed, optional 16-byte personalization.
+// Used for the Sprout hSig (personal "ZcashComputehSig", verification/src/sprout.rs:16-32),
+// seeded-mode batch scalars and synthetic re-randomization scalars (the product's production
+// mode draws r_i from the OS RNG).
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -19,9 +20,16 @@ struct Blake2b {
                                      0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
                                      0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
 
-  explicit Blake2b(size_t out) : t(0), n(0), outlen(out) {
+  explicit Blake2b(size_t out, const uint8_t* personal = nullptr) : t(0), n(0), outlen(out) {
     for (int i = 0; i < 8; i++) h[i] = IV[i];
     h[0] ^= 0x01010000ull ^ (uint64_t)out;
+    if (personal) {  // parameter block bytes 48..63
+      for (int w = 0; w < 2; w++) {
+        uint64_t v = 0;
+        for (int b = 7; b >= 0; b--) v = (v << 8) | personal[8 * w + b];
+        h[6 + w] ^= v;
+      }
+    }
   }
   void compress(bool last) {
     static const uint8_t S[12][16] = {

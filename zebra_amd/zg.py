@@ -57,8 +57,63 @@ def lib():
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
         L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
+        L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
+        L.zg_prep_joinsplit.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
+        L.zg_hsig.argtypes = [u8p, u8p, u8p, u8p, u8p]
         _lib = L
     return _lib
+
+
+# ---- host-side public-input preparation (include/zg.h zg_prep_*; CPU, no GPU needed)
+PREP_ERRORS = {1: "ValueCommitment(Invalid)", 2: "ValueCommitment(SmallOrder)", 3: "Anchor",
+               4: "RandomizedKey(Invalid)", 5: "RandomizedKey(SmallOrder)", 6: "NoteCommitment",
+               7: "EphemeralKey(Invalid)", 8: "EphemeralKey(SmallOrder)"}
+
+
+class PrepError(ValueError):
+    """a description's public input failed the reference's checks (SpendError/OutputError class)"""
+
+    def __init__(self, code):
+        super().__init__(PREP_ERRORS.get(code, str(code)))
+        self.code = code
+        self.name = PREP_ERRORS.get(code, str(code))
+
+
+def _prep(rc, out, n):
+    if rc < 0:
+        raise ZgError(rc, "bad argument")
+    if rc:
+        raise PrepError(rc)
+    return [out.raw[32 * j:32 * j + 32] for j in range(n)]
+
+
+def prep_spend(cv, anchor, nullifier, rk):
+    """accept_spend (verification/src/sapling.rs:101-155) -> 7 x 32-byte LE Fr"""
+    out = ctypes.create_string_buffer(7 * 32)
+    return _prep(lib().zg_prep_spend(bytes(cv), bytes(anchor), bytes(nullifier), bytes(rk), out), out, 7)
+
+
+def prep_output(cv, cmu, epk):
+    """accept_output (verification/src/sapling.rs:171-200) -> 5 x 32-byte LE Fr"""
+    out = ctypes.create_string_buffer(5 * 32)
+    return _prep(lib().zg_prep_output(bytes(cv), bytes(cmu), bytes(epk), out), out, 5)
+
+
+def prep_joinsplit(anchor, random_seed, nullifiers, macs, commitments, vpub_old, vpub_new, pubkey):
+    """sprout::verify input (verification/src/sprout.rs:34-58,86-153) -> 9 x 32-byte LE Fr"""
+    out = ctypes.create_string_buffer(9 * 32)
+    return _prep(lib().zg_prep_joinsplit(bytes(anchor), bytes(random_seed), b"".join(map(bytes, nullifiers)),
+                                         b"".join(map(bytes, macs)), b"".join(map(bytes, commitments)),
+                                         vpub_old, vpub_new, bytes(pubkey), out), out, 9)
+
+
+def hsig(random_seed, nf0, nf1, pubkey):
+    out = ctypes.create_string_buffer(32)
+    rc = lib().zg_hsig(bytes(random_seed), bytes(nf0), bytes(nf1), bytes(pubkey), out)
+    if rc:
+        raise ZgError(rc, "bad argument")
+    return out.raw
 
 
 def pack_inputs(rows):
