@@ -21,11 +21,14 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# frozen algorithmic work per proof (Fq-mul-equivalents), split per kernel.
-W_DECODE = 2679 + 2 * 507 + 1189 + 1593 + 264 + 3   # K1 decode+subgroup, K2 Fr, K3 r_i A_i, K4 MSM share
-W_MILLER = 1634 + 5192                              # K5 G2 lines + K6 Miller loop
-W_TREE = 54                                         # tree-product Fq12 multiply
+# frozen algorithmic work per proof (Fq-mul-equivalents), attributed to the
+# kernel that performs it (the G2 subgroup check of B rides on the R-chain kernel).
+W_DECODE = 2679 + 2 * 507 + 1593 + 264 + 3   # point decode (2 Fq + 1 Fq2 sqrt), 2 G1 checks, r_i A_i, MSM share, Fr
+W_LINES = 1634 + 1189                        # G2 line coefficients (R-chain) + G2 subgroup check
+W_FCHAIN = 5192                              # Miller f-chain (sparse line products + squarings)
+W_TREE = 54                                  # tree-product Fq12 multiply
 W_TOTAL = 13622
+assert W_DECODE + W_LINES + W_FCHAIN + W_TREE == W_TOTAL
 MACS_PER_FQMUL = 288                                # 2 * 12^2 32x32->64 MACs (product + CIOS reduction)
 
 
@@ -76,6 +79,62 @@ def cpu_baseline(proofs, kinds, inputs, seconds, threads):
                       "%.1f s" % (m, dt)}
 
 
+def other_configs(ctx, src_proofs, src_kinds, reps=5):
+    """SURVEY.md 8(d) configs 2 and 4 through the host-buffer API zg_verify_batch (PCIe copies,
+    OS-RNG scalars and the exact per-proof statuses included): not the headline metric."""
+    import random
+    real = {e["name"]: e for e in json.load(open(os.path.join(ROOT, "tests", "golden", "real_proofs.json")))["proofs"]}
+    pts = json.load(open(os.path.join(ROOT, "tests", "golden", "points.json")))
+    srcs = ["S1", "S2", "O1", "O2", "O3"]
+    rows = {s: [bytes.fromhex(x) for x in real[s]["inputs"]] for s in srcs}
+    from zebra_amd import pack_inputs
+    res = {}
+    # config 2: 1,024 spends, proof i = S[i mod 2] re-randomized with seed 1
+    idx = [i % 2 for i in range(1024)]
+    proofs = ctx.synth_rerandomize(src_proofs, src_kinds, idx, 1)
+    kinds = bytes(src_kinds[j] for j in idx)
+    inputs = pack_inputs([rows[srcs[j]] for j in idx])
+    ctx.verify_batch(proofs, kinds, inputs)
+    t = time.perf_counter()
+    for _ in range(reps):
+        sts, _ = ctx.verify_batch(proofs, kinds, inputs)
+    dt = (time.perf_counter() - t) / reps
+    assert sts == [0] * 1024
+    res["config2_1024_spends"] = {"proofs_per_s": 1024 / dt, "ms_per_batch": dt * 1e3, "all_ok": True}
+    # config 4: 4,096 mixed, 41 corrupted (seed 3) -> exact reject set via bisection
+    n = 4096
+    idx = [i % 5 for i in range(n)]
+    proofs = bytearray(ctx.synth_rerandomize(src_proofs, src_kinds, idx, 3))
+    rowsl = [list(rows[srcs[j]]) for j in idx]
+    rng = random.Random(3)
+    bad = sorted(rng.sample(range(n), 41))
+    want = [0] * n
+    for q, i in enumerate(bad):
+        if q % 3 == 0:
+            x = bytearray(rowsl[i][0])
+            x[0] ^= 1
+            rowsl[i][0] = bytes(x)
+            want[i] = 3
+        elif q % 3 == 1:
+            p = proofs[192 * i:192 * i + 192]
+            proofs[192 * i:192 * i + 192] = p[144:] + p[48:144] + p[:48]
+            want[i] = 3
+        else:
+            proofs[192 * i + 48:192 * i + 144] = bytes.fromhex(pts["g2_not_in_subgroup"])
+            want[i] = 1
+    kinds = bytes(src_kinds[j] for j in idx)
+    inputs = pack_inputs(rowsl)
+    ctx.verify_batch(bytes(proofs), kinds, inputs)
+    t = time.perf_counter()
+    for _ in range(reps):
+        sts, _ = ctx.verify_batch(bytes(proofs), kinds, inputs)
+    dt = (time.perf_counter() - t) / reps
+    assert sts == want, "config 4 reject set differs"
+    res["config4_4096_1pct_corrupted"] = {"proofs_per_s": n / dt, "ms_per_batch": dt * 1e3, "rejected": len(bad),
+                                          "exact_reject_set": True}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,6 +142,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=65536, help="total proofs per step (all ranks)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 side measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -144,10 +204,11 @@ def main():
 
     total = shard * world
     value = total * args.steps / dt
-    names = ["k_batch_decode", "k_batch_miller", "k_tree_f", "root_partial", "side_stream_vk", "device_pipeline"]
-    avg = [sum(t[i] for t in timings) / len(timings) for i in range(6)]
+    names = ["k_batch_decode", "k_batch_lines", "k_batch_fchain", "k_tree_f", "root_partial", "side_stream_vk",
+             "device_pipeline"]
+    avg = [sum(t[i] for t in timings) / len(timings) for i in range(7)]
     dom = max(range(3), key=lambda i: avg[i])
-    wk = {0: W_DECODE, 1: W_MILLER, 2: W_TREE}[dom]
+    wk = {0: W_DECODE, 1: W_LINES, 2: W_FCHAIN}[dom]
     achieved = wk * MACS_PER_FQMUL * shard / (avg[dom] * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -168,6 +229,8 @@ def main():
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
     }
+    if rank == 0 and world == 1 and not args.no_configs:
+        out["other_configs"] = other_configs(ctx, src_proofs, src_kinds)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(proofs, kinds, inputs, args.cpu_seconds,
                                            min(args.cpu_threads, os.cpu_count() or 1))

@@ -163,10 +163,11 @@ int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, c
 
 /* ---- measurement helpers */
 /* time (ms, HIP events on the context streams) of the most recent zg_batch_begin* +
- * zg_batch_partial: [0] decode (main stream), [1] per-proof Miller loops, [2] Fq12 product
- * tree, [3] root partial, [4] side stream (C/Fr trees + VK-side MSM + VK Miller loops,
- * overlapping [1]-[2]), [5] whole device pipeline */
-int zg_last_timings(zg_ctx* ctx, float* ms6);
+ * zg_batch_partial: [0] decode (main stream), [1] R-chain / line coefficients (+ G2 subgroup
+ * checks), [2] f-chain (per-proof Miller values), [3] Fq12 product tree, [4] root partial,
+ * [5] side stream (C/Fr trees + VK-side MSM + VK Miller loops, overlapping [2]-[3]),
+ * [6] whole device pipeline */
+int zg_last_timings(zg_ctx* ctx, float* ms7);
 /* microbenchmark: v_mad_u64_u32 chains; returns achieved 32x32->64 MACs per second */
 int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s);
 

@@ -22,6 +22,7 @@ using namespace zg;
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 8
+#define ZG_NTIMINGS 7
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 
 struct zg_ctx {
@@ -59,7 +60,7 @@ struct zg_ctx {
   hipStream_t side = nullptr;  // VK-side root work, concurrent with the Miller kernel
   int root_pairs_ready = 0;     // the pipeline already ran the root's MSM + VK pairs on `side`
   hipEvent_t ev[ZG_NEV] = {};
-  float timings[6] = {0, 0, 0, 0, 0, 0};
+  float timings[ZG_NTIMINGS] = {};
   uint64_t calls = 0;
 };
 
@@ -358,29 +359,34 @@ static BatchBufs batch_bufs(zg_ctx* ctx) {
   b.ftree = ctx->d_ftree;
   b.ctree = ctx->d_ctree;
   b.stree = ctx->d_stree;
+  b.bfail = ctx->d_int + 8;
   b.n = (int)ctx->n;
   b.npad = (int)ctx->npad;
   return b;
 }
 
-static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs& nb, hipStream_t st) {
+static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs& nb, hipStream_t st,
+                                 const int* gate = nullptr) {
   hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS)), dim3(ZG_BLOCK),
-                     0, st, b, nb);
+                     0, st, b, nb, gate);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, st, b, nb);
+  hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, st, b, nb, gate);
   HIPCHK(hipGetLastError());
   return ZG_OK;
 }
 
 // The pipeline on device-resident inputs already in ctx buffers.
-//   main stream: decode -> Miller -> Fq12 product tree
+//   main stream: decode -> R-chain (lines + G2 subgroup checks) -> f-chain -> Fq12 product tree
 //   side stream: (after decode) C / Fr sum trees -> root VK-side MSM -> root VK Miller loops
-// The side stream only needs the decode results, so its serial, few-thread work overlaps the
-// full-GPU Miller kernel instead of extending the critical path.
+// The side stream only needs the decode results, so its few-thread work overlaps the lines
+// and f-chain kernels instead of extending the critical path. A B_i that fails its G2
+// subgroup check in k_batch_lines (invalid proofs only) counts in bfail, and the side-stream
+// results are then recomputed on the main stream (gated kernels: no-ops when bfail == 0).
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   static const int root = 1;
   HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemsetAsync(b.bfail, 0, sizeof(int), ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   // one wave per 64 proofs fills every SIMD from 64k proofs up; below, split the chains
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
@@ -394,17 +400,18 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->side));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo);
+    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo, (const int*)nullptr);
     HIPCHK(hipGetLastError());
   }
   NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
   int rc = launch_node_msm_pairs(ctx, b, nb, ctx->side);
   if (rc) return rc;
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->side));
-  // main stream: per-proof Miller loops as the R-chain (lines) + f-chain programs
+  // main stream: the R-chain (lines; also the G2 subgroup checks of the B_i), then the f-chain
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
   hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
   hipLaunchKernelGGL(k_batch_fchain, dim3(groups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
@@ -415,8 +422,16 @@ static int run_pipeline(zg_ctx* ctx) {
       hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream trees + root pairs complete
+  // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
+  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
+    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo,
+                       (const int*)b.bfail);
+    HIPCHK(hipGetLastError());
+  }
+  rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
+  if (rc) return rc;
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // trees + root pairs complete
   ctx->root_pairs_ready = 1;
   return ZG_OK;
 }
@@ -534,9 +549,13 @@ extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
   int rc = check_nodes(ctx, root, 1, nullptr, partial);
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
-  for (int i = 0; i < 4; i++) hipEventElapsedTime(&ctx->timings[i], ctx->ev[i], ctx->ev[i + 1]);
-  hipEventElapsedTime(&ctx->timings[4], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
-  hipEventElapsedTime(&ctx->timings[5], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
+  hipEventElapsedTime(&ctx->timings[0], ctx->ev[0], ctx->ev[1]);  // decode
+  hipEventElapsedTime(&ctx->timings[1], ctx->ev[1], ctx->ev[7]);  // lines (R-chain)
+  hipEventElapsedTime(&ctx->timings[2], ctx->ev[7], ctx->ev[2]);  // f-chain
+  hipEventElapsedTime(&ctx->timings[3], ctx->ev[2], ctx->ev[3]);  // Fq12 product tree
+  hipEventElapsedTime(&ctx->timings[4], ctx->ev[3], ctx->ev[4]);  // root partial (after the side stream)
+  hipEventElapsedTime(&ctx->timings[5], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
+  hipEventElapsedTime(&ctx->timings[6], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
   return rc;
 }
 
@@ -625,9 +644,9 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
   return zg_batch_finish(ctx, ok, status);
 }
 
-extern "C" int zg_last_timings(zg_ctx* ctx, float* ms6) {
-  if (!ctx || !ms6) return ZG_E_INVAL;
-  for (int i = 0; i < 6; i++) ms6[i] = ctx->timings[i];
+extern "C" int zg_last_timings(zg_ctx* ctx, float* ms7) {
+  if (!ctx || !ms7) return ZG_E_INVAL;
+  for (int i = 0; i < ZG_NTIMINGS; i++) ms7[i] = ctx->timings[i];
   return ZG_OK;
 }
 

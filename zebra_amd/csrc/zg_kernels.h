@@ -33,6 +33,7 @@ struct BatchBufs {
   Fq12* ftree;             // 2 npad
   G1J* ctree;              // 2 npad x 3 kinds
   Fr* stree;               // 2 npad x 3 kinds x ZG_MAX_IC (Montgomery)
+  int* bfail;              // count of B_i failing the (deferred) G2 subgroup check
   int n, npad;
 };
 
@@ -40,7 +41,8 @@ struct BatchBufs {
 // r_i C_i and the Fr scalars r_i, r_i x_ij as tree leaves. Lane = proof; a block = 64 proofs.
 // Three independent chains per proof:
 //   A: Fq sqrt, G1 subgroup check, [r_i] A_i by GLV columns, to affine
-//   B: Fq2 sqrt, G2 subgroup check; public inputs, status, Fr scalar leaves
+//   B: Fq2 sqrt (its G2 subgroup check rides on k_batch_lines); public inputs, status, Fr
+//      scalar leaves
 //   C: Fq sqrt, G1 subgroup check, [r_i] C_i by GLV columns
 // W = 1: one wave runs all three (a 64k batch already puts one wave on every SIMD);
 // W = 3: one wave per chain, for small batches / shards (3x the waves, ~1/3 the latency).
@@ -69,7 +71,8 @@ __global__ void __launch_bounds__(64 * W) k_batch_decode(BatchBufs b) {
       k = b.ninputs ? b.ninputs[i] : KIND_NINPUTS[kind];
       kk = k < ZG_MAX_INPUTS ? k : ZG_MAX_INPUTS;
       if (!inputs_canonical(b.inputs + (size_t)i * 288, kk, x)) st_in = ST_INPUT_NONCANONICAL;
-      okb = g2_decompress(b.proofs + (size_t)i * 192 + 48, &q) == DEC_OK;
+      // the G2 subgroup check of B is fused into k_batch_lines: the R-chain ends at [x] B
+      okb = g2_decompress(b.proofs + (size_t)i * 192 + 48, &q, false) == DEC_OK;
     }
   }
   if (runA) {
@@ -111,8 +114,12 @@ __global__ void __launch_bounds__(64 * W) k_batch_decode(BatchBufs b) {
     if (inb) b.ptA[i] = o;
   }
   if (runC && pend) b.ctree[leaf * ZG_NKINDS + kind] = g1_glv_mul(pc, ra, rb);
+  if (runB && inb) {  // B still owes its subgroup check (k_batch_lines) if Proof::read got that far
+    G2A qq = q;
+    qq.inf = !(live && (st == ST_PENDING || st == ST_MALFORMED_VK));
+    b.ptB[i] = qq;
+  }
   if (runB && pend) {
-    b.ptB[i] = q;
     const Fr rf = batch_scalar_fr(ra, rb);
     Fr* s = b.stree + (leaf * ZG_NKINDS + kind) * ZG_MAX_IC;
     s[0] = rf;
@@ -146,20 +153,27 @@ __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
 
 // lines layout: [step][proof][A, B, C]
 // LDS slots (both programs): 0 X, 1 Y, 2 Z, 3 PQ = (px, py) (kept), add: 4 QX, 5 QY
+// The R-chain of pairing's G2Prepared is the double-and-add of [x] B (x = |u|, Jacobian), so
+// the G2 subgroup check of B (psi(B) = [u] B, zg_curve.h) is its last step here: a B that
+// fails it turns its proof DECODE_INVALID (Proof::read) and its leaves back to the identity.
 __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
   const AtomSpace at{lds_atoms};
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const int proof = blockIdx.x * 64 + lane;
   const bool act = proof_active(b, proof);
+  const bool chk = proof < b.n && !b.ptB[proof].inf;  // B owes its subgroup check
   if (wave == 0) {
     G2A q;
     G1A p;
-    if (act) {
+    if (chk) {
       q = b.ptB[proof];
-      p = b.ptA[proof];
     } else {
       q.x = q.y = f2_one();
+    }
+    if (act) {
+      p = b.ptA[proof];
+    } else {
       p.x = p.y = fq_one();
     }
     at.put(0, q.x);
@@ -175,8 +189,8 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
       const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
       if (pid == ZG_PROG_ADD) {
         if (wave < 2) {
-          const G2A q = b.ptB[act ? proof : 0];
-          at.put(4 + wave, wave == 0 ? (act ? q.x : f2_one()) : (act ? q.y : f2_one()));
+          const G2A q = b.ptB[chk ? proof : 0];
+          at.put(4 + wave, wave == 0 ? (chk ? q.x : f2_one()) : (chk ? q.y : f2_one()));
         }
         __syncthreads();
       }
@@ -190,6 +204,23 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
         lines[((size_t)n * b.npad + proof) * 3 + (wave - 3)] = act ? v : f2_one();
       __syncthreads();
       n++;
+    }
+  }
+  // R = [x] B (Jacobian). B in G2  <=>  psi(B) = [u] B = -[x] B  <=>  X = psi_x Z^2, Y = -psi_y Z^3,
+  // Z != 0 (pairing's step formulas are exact unless they degenerate, which only a B outside
+  // G2 can make happen, and then Z = 0)
+  if (wave == 0 && chk) {
+    const G2A q = b.ptB[proof];
+    const Fq2 X = at.get(0), Y = at.get(1), Z = at.get(2);
+    const G2A s = g2_psi(q);
+    const Fq2 z2 = f2_sqr(Z), z3 = f2_mul(z2, Z);
+    const bool in_g2 = !f2_is_zero(Z) && f2_eq(X, f2_mul(s.x, z2)) && f2_eq(Y, f2_neg(f2_mul(s.y, z3)));
+    if (!in_g2) {
+      atomicAdd(b.bfail, 1);
+      b.status[proof] = ST_DECODE_INVALID;
+      const int leaf = b.npad + proof, kind = b.kinds[proof];
+      b.ctree[leaf * ZG_NKINDS + kind] = jac_infinity<Fq>();
+      for (int m = 0; m < ZG_MAX_IC; m++) b.stree[(leaf * ZG_NKINDS + kind) * ZG_MAX_IC + m] = fp_zero<FrM>();
     }
   }
 }
@@ -259,7 +290,9 @@ __global__ void __launch_bounds__(64) k_tree_f_coop(BatchBufs b, int lo) {
 
 // C-sum and Fr scalar-sum tree level (depends on k_batch_decode only, so it runs on the
 // side stream concurrently with the Miller kernel)
-__global__ void __launch_bounds__(64) k_tree_cs(BatchBufs b, int lo) {
+// gate: null = always; else run only if *gate != 0 (the recompute after a deferred B failure)
+__global__ void __launch_bounds__(64) k_tree_cs(BatchBufs b, int lo, const int* gate) {
+  if (gate && *gate == 0) return;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= lo) return;
   const int node = lo + j, l = 2 * node, r = 2 * node + 1;
@@ -282,7 +315,8 @@ struct NodeBufs {
 
 // VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k, each 255-bit scalar
 // split into 8 x 32-bit chunks against the pre-shifted bases [2^(32 w)] base (8 threads).
-__global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb) {
+__global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb, const int* gate) {
+  if (gate && *gate == 0) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS) return;
   const int w = t % ZG_SHIFTS;
@@ -340,7 +374,8 @@ __device__ void coop_miller_prepared(CoopWS* ws, const Fq& px, const Fq& py, con
 }
 
 // VK-side Miller loops per checked node: one wave per (node, kind, pair)
-__global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb) {
+__global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb, const int* gate) {
+  if (gate && *gate == 0) return;
   __shared__ CoopWS ws;
   __shared__ Fq px, py;
   __shared__ const Line* lines;
@@ -352,29 +387,46 @@ __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb) {
   const int pair = t % ZG_NPAIRS;
   const int node = nb.nodes[idx];
   const DevVK& vk = b.vks[kind];
+  // the G1 point of this pair: the sum of up to 80 MSM partials (gamma pair), 8 (beta pair) or
+  // the batch's C sum (delta pair) -- summed across the wave (one add per lane + 6 LDS levels)
+  __shared__ G1J red[64];
+  const int lane = threadIdx.x & 63;
+  const G1J* ms = nb.msm + (size_t)(idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS * ZG_SHIFTS;
+  int cnt = 0, off = 0;
+  const Line* ln = nullptr;
+  if (vk.loaded) {
+    if (pair == 0 && !vk.gamma.inf) {
+      cnt = vk.ic_len * ZG_SHIFTS;
+      ln = vk.neg_gamma_lines;
+    } else if (pair == 1 && !vk.delta.inf) {
+      ln = vk.neg_delta_lines;
+    } else if (pair == 2 && !vk.beta.inf) {
+      cnt = ZG_SHIFTS;
+      off = ZG_MAX_IC * ZG_SHIFTS;
+      ln = vk.beta_lines;
+    }
+  }
+  G1J acc = jac_infinity<Fq>();
+  if (pair == 1) {
+    if (lane == 0) acc = b.ctree[node * ZG_NKINDS + kind];
+  } else {
+    if (lane < cnt) acc = ms[off + lane];
+    if (lane + 64 < cnt) acc = jac_add(acc, ms[off + lane + 64]);
+  }
+  red[lane] = acc;
+  __syncthreads();
+  for (int s = 32; s >= 1; s >>= 1) {
+    if (lane < s) red[lane] = jac_add(red[lane], red[lane + s]);
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
     lines = nullptr;
-    if (vk.loaded) {
-      const G1J* ms = nb.msm + (size_t)(idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS * ZG_SHIFTS;
-      G1J pj = jac_infinity<Fq>();
-      const Line* ln = nullptr;
-      if (pair == 0 && !vk.gamma.inf) {
-        for (int j = 0; j < vk.ic_len * ZG_SHIFTS; j++) pj = jac_add(pj, ms[j]);
-        ln = vk.neg_gamma_lines;
-      } else if (pair == 1 && !vk.delta.inf) {
-        pj = b.ctree[node * ZG_NKINDS + kind];
-        ln = vk.neg_delta_lines;
-      } else if (pair == 2 && !vk.beta.inf) {
-        for (int w = 0; w < ZG_SHIFTS; w++) pj = jac_add(pj, ms[ZG_MAX_IC * ZG_SHIFTS + w]);
-        ln = vk.beta_lines;
-      }
-      if (ln) {
-        G1A p = jac_to_aff(pj);
-        if (!p.inf) {
-          px = p.x;
-          py = p.y;
-          lines = ln;
-        }
+    if (ln) {
+      G1A p = jac_to_aff(red[0]);
+      if (!p.inf) {
+        px = p.x;
+        py = p.y;
+        lines = ln;
       }
     }
   }

@@ -226,7 +226,8 @@ class Context:
         return list(st.raw[:n])
 
     def last_timings(self):
-        a = (ctypes.c_float * 6)()
+        """[decode, lines, fchain, tree, root_partial, side_stream, device_pipeline] in ms"""
+        a = (ctypes.c_float * 7)()
         self._chk(lib().zg_last_timings(self._p, a))
         return list(a)
 
