@@ -126,7 +126,7 @@ ZG_INL Jac<F> jac_add_aff_inl(const Jac<F>& p, const Aff<F>& q) {
   F H = F_sub(U2, p.x);
   F rr = F_dbl(F_sub(S2, p.y));
   if (F_is_zero(H)) {
-    if (F_is_zero(rr)) return jac_dbl(p);
+    if (F_is_zero(rr)) return jac_dbl_inl(p);  // inlined: no pointer to p (keeps p out of scratch)
     return jac_infinity<F>();
   }
   F HH = F_sqr(H);
@@ -154,9 +154,9 @@ template <class F>
 ZG_NOINL void jac_mul_limbs_p(Jac<F>* out, const Aff<F>* qp, const uint32_t* k, int nbits) {
   const Aff<F> q = *qp;
   Jac<F> acc = jac_infinity<F>();
-  for (int i = nbits - 1; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff(acc, q);
+  for (int i = nbits - 1; i >= 0; i--) {  // point ops inlined: acc stays in registers
+    acc = jac_dbl_inl(acc);
+    if ((k[i >> 5] >> (i & 31)) & 1u) acc = jac_add_aff_inl(acc, q);
   }
   *out = acc;
 }
@@ -193,8 +193,13 @@ ZG_INL bool jac_eq_aff(const Jac<F>& p, const Aff<F>& q) {
 // ------------------------------------------------------------------ subgroup checks
 ZG_NOINL inline bool g1_in_subgroup(const G1A& p) {
   if (p.inf) return true;
-  // [x^2] P  with x^2 < 2^128 (positive), then sigma(P) == -[x^2]P
-  G1J q = jac_mul_limbs(p, X2_ABS, 128);
+  // [x^2] P  with x^2 < 2^128 (positive), then sigma(P) == -[x^2]P; the point ops are inlined
+  // so the Jacobian state stays in registers (the exponent is uniform: no divergence)
+  G1J q = jac_from_aff(p);
+  for (int i = 126; i >= 0; i--) {  // bit 127 of x^2 is the leading one
+    q = jac_dbl_inl(q);
+    if ((X2_ABS[i >> 5] >> (i & 31)) & 1u) q = jac_add_aff_inl(q, p);
+  }
   G1A s = {fq_mul(p.x, fq_const(G1_BETA)), fq_neg(p.y), false};
   return jac_eq_aff(q, s);
 }

@@ -130,11 +130,12 @@ ZG_NOINL inline void g1_glv_mul_p(G1J* out, const G1A* pp, uint64_t a, uint64_t 
   }
   const bool etop = k1 & 1u;  // k1 is 0 or 1 here
   G1J q = {etop ? bx : p.x, etop ? ny : p.y, fq_one()};
+  // dbl + madd inlined: the Jacobian state stays in registers across the out-of-line fq_mul
+  // leaf calls (passing it by pointer to noinline point ops sent it through scratch)
   for (int j = 63; j >= 0; j--) {
-    q = jac_dbl(q);
     const bool ej = (e >> j) & 1u, neg = !((a >> j) & 1u);
     const G1A t = {ej ? bx : p.x, (ej != neg) ? ny : p.y, false};
-    q = jac_add_aff(q, t);
+    q = jac_add_aff_inl(jac_dbl_inl(q), t);
   }
   *out = q;
 }

@@ -479,17 +479,17 @@ __global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, int co
   if (threadIdx.x == 0) *ok = one ? 1 : 0;
 }
 
-__global__ void k_f12_to_bytes(const Fq12* a, int count, uint8_t* out) {
+__global__ void __launch_bounds__(64) k_f12_to_bytes(const Fq12* a, int count, uint8_t* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < count) f12_to_bytes(a[i], out + (size_t)576 * i);
 }
-__global__ void k_f12_from_bytes(const uint8_t* in, int count, Fq12* a) {
+__global__ void __launch_bounds__(64) k_f12_from_bytes(const uint8_t* in, int count, Fq12* a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < count) a[i] = f12_from_bytes(in + (size_t)576 * i);
 }
 
 // prepare_verifying_key (one thread)
-__global__ void k_vk_prepare(const RawVK* raw, DevVK* vk, int* err) {
+__global__ void __launch_bounds__(64) k_vk_prepare(const RawVK* raw, DevVK* vk, int* err) {
   if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
   *err = vk_prepare(*raw, vk);
 }
