@@ -68,7 +68,8 @@ extern "C" {
 typedef struct zg_config {
   int device;         /* HIP device ordinal (one process per GPU) */
   uint32_t max_batch; /* capacity of one batch (proofs); 0 -> 65536 */
-  int seeded;         /* 1: batch scalars r_i from BLAKE2b(seed, i) (tests); 0: OS RNG */
+  int seeded;         /* 1: batch scalars r_i from BLAKE2b(seed, i) (tests); 0: OS-random
+                         ChaCha20 key per batch, expanded on the GPU (zg_chacha20_blocks) */
   uint64_t seed;
 } zg_config;
 
@@ -168,6 +169,12 @@ int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, c
  * [5] side stream (C/Fr trees + VK-side MSM + VK Miller loops, overlapping [2]-[3]),
  * [6] whole device pipeline */
 int zg_last_timings(zg_ctx* ctx, float* ms7);
+/* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
+ * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.
+ * This entry runs the same device block function for known-answer tests: out = nblocks x 64 B
+ * of the keystream for (key, nonce) from block `counter` on. */
+int zg_chacha20_blocks(zg_ctx* ctx, const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                       size_t nblocks, uint8_t* out);
 /* microbenchmark: v_mad_u64_u32 chains; returns achieved 32x32->64 MACs per second */
 int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s);
 

@@ -13,6 +13,7 @@
 
 #include "../../include/zg.h"
 #include "zg_blake2b.h"
+#include "zg_chacha.h"
 #include "zg_kernels.h"
 #include "zg_prep.h"
 #include "zg_vk_embed.h"  // generated from zebra_amd/res/*.json by zebra_amd/build.py
@@ -103,7 +104,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
        dalloc(&ctx->d_int, 16) == hipSuccess;
   ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
        dalloc(&ctx->d_inputs, (size_t)cap * 288) == hipSuccess && dalloc(&ctx->d_ninputs, cap) == hipSuccess &&
-       dalloc(&ctx->d_r, (size_t)cap * 16) == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
+       dalloc(&ctx->d_r, ((size_t)cap + 3) / 4 * 64)  /* whole ChaCha20 blocks */ == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
        dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
   ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
        dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
@@ -331,18 +332,44 @@ static void gen_scalars(zg_ctx* ctx, size_t n, std::vector<uint8_t>& r) {
       h.update(le, 8);
       h.final(&r[16 * i]);
     }
-  } else {
-    size_t off = 0;
-    while (off < r.size()) {
-      ssize_t got = getrandom(&r[off], r.size() - off, 0);
-      if (got < 0) {
-        if (errno == EINTR) continue;
-        break;
-      }
-      off += (size_t)got;
-    }
   }
   // any 16 bytes are a valid batch scalar: r_i = (2a + 1) + b lambda != 0 (zg_groth16.h)
+}
+
+static bool os_random(void* buf, size_t len) {
+  uint8_t* p = (uint8_t*)buf;
+  size_t off = 0;
+  while (off < len) {
+    ssize_t got = getrandom(p + off, len - off, 0);
+    if (got < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    off += (size_t)got;
+  }
+  return true;
+}
+
+// r_i of the current batch into d_r. Seeded contexts (tests) derive them on the host
+// (BLAKE2b(seed, i), see gen_scalars); otherwise one fresh 256-bit OS-random ChaCha20 key per
+// batch is expanded on the device: 4 proofs per 64-byte block, no host round trip.
+static int stage_scalars(zg_ctx* ctx, size_t n) {
+  if (!n) return ZG_OK;
+  if (ctx->seeded) {
+    std::vector<uint8_t> rr;
+    gen_scalars(ctx, n, rr);
+    HIPCHK(hipMemcpyAsync(ctx->d_r, rr.data(), n * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return ZG_OK;
+  }
+  ChachaKey k;
+  if (!os_random(k.key, sizeof(k.key))) return fail(ctx, ZG_E_INVAL, "getrandom failed");
+  k.nonce[0] = k.nonce[1] = k.nonce[2] = 0;  // the key is single-use
+  const size_t nb = (n + 3) / 4;
+  hipLaunchKernelGGL(k_chacha20, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, ctx->stream, k, 0u, nb,
+                     (uint4*)ctx->d_r);
+  HIPCHK(hipGetLastError());
+  return ZG_OK;
 }
 
 static BatchBufs batch_bufs(zg_ctx* ctx) {
@@ -375,6 +402,17 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
   return ZG_OK;
 }
 
+namespace zg {  // zg_decode.hip
+hipError_t launch_batch_decode(int w, unsigned groups, hipStream_t st, const BatchBufs& b);
+}
+static int decode_waves() {
+  static const int w = [] {
+    const char* e = getenv("ZG_DECODE_W");
+    return e && atoi(e) == 3 ? 3 : 1;
+  }();
+  return w;
+}
+
 // The pipeline on device-resident inputs already in ctx buffers.
 //   main stream: decode -> R-chain (lines + G2 subgroup checks) -> f-chain -> Fq12 product tree
 //   side stream: (after decode) C / Fr sum trees -> root VK-side MSM -> root VK Miller loops
@@ -388,13 +426,9 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemsetAsync(b.bfail, 0, sizeof(int), ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  // one wave per 64 proofs fills every SIMD from 64k proofs up; below, split the chains
+  // one wave per chain (A, B, C) of 64 proofs, two waves per SIMD (zg_decode.hip)
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
-  if (dgroups >= 1024)
-    hipLaunchKernelGGL(k_batch_decode<1>, dim3(dgroups), dim3(64), 0, ctx->stream, b);
-  else
-    hipLaunchKernelGGL(k_batch_decode<3>, dim3(dgroups), dim3(192), 0, ctx->stream, b);
-  HIPCHK(hipGetLastError());
+  HIPCHK(launch_batch_decode(decode_waves(), dgroups, ctx->stream, b));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   // side stream
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
@@ -463,16 +497,14 @@ extern "C" int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, cons
   int rc = begin_common(ctx, n);
   if (rc) return rc;
   if ((rc = check_kinds(ctx, n, kinds))) return rc;
-  std::vector<uint8_t> rr;
-  if (!r) {
-    gen_scalars(ctx, n, rr);
-    r = rr.data();
-  }
   if (n) {
     HIPCHK(hipMemcpyAsync(ctx->d_proofs, proofs, n * 192, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(ctx->d_kinds, kinds, n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(ctx->d_inputs, inputs, n * 288, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_r, r, n * 16, hipMemcpyHostToDevice, ctx->stream));
+    if (r)
+      HIPCHK(hipMemcpyAsync(ctx->d_r, r, n * 16, hipMemcpyHostToDevice, ctx->stream));
+    else if ((rc = stage_scalars(ctx, n)))
+      return rc;
     if (n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, n_inputs, n, hipMemcpyHostToDevice, ctx->stream));
   }
   ctx->cur_ninputs = n_inputs ? ctx->d_ninputs : nullptr;
@@ -499,11 +531,8 @@ extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs
     HIPCHK(hipMemcpyAsync(ctx->d_inputs, d_inputs, n * 288, hipMemcpyDeviceToDevice, ctx->stream));
     if (d_r) {
       HIPCHK(hipMemcpyAsync(ctx->d_r, d_r, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
-    } else {
-      std::vector<uint8_t> rr;
-      gen_scalars(ctx, n, rr);
-      HIPCHK(hipMemcpyAsync(ctx->d_r, rr.data(), n * 16, hipMemcpyHostToDevice, ctx->stream));
-      HIPCHK(hipStreamSynchronize(ctx->stream));
+    } else if ((rc = stage_scalars(ctx, n))) {
+      return rc;
     }
     if (d_n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, d_n_inputs, n, hipMemcpyDeviceToDevice, ctx->stream));
   }
@@ -774,5 +803,27 @@ extern "C" int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s) {
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
   *macs_per_s = (double)blocks * threads * iters * 64.0 / (ms * 1e-3);
+  return ZG_OK;
+}
+
+// ChaCha20 blocks on the device (the batch-scalar CSPRNG), for known-answer tests
+extern "C" int zg_chacha20_blocks(zg_ctx* ctx, const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                                  size_t nblocks, uint8_t* out) {
+  if (!ctx || !key || !nonce || (nblocks && !out)) return ZG_E_INVAL;
+  if (!nblocks) return ZG_OK;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  ChachaKey k;
+  memcpy(k.key, key, 32);
+  memcpy(k.nonce, nonce, 12);
+  uint4* d = nullptr;
+  HIPCHK(hipMalloc(&d, 64 * nblocks));
+  hipLaunchKernelGGL(k_chacha20, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, ctx->stream, k, counter,
+                     nblocks, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, 64 * nblocks, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  if (e != hipSuccess) return fail(ctx, ZG_E_HIP, std::string("zg_chacha20_blocks: ") + hipGetErrorString(e));
   return ZG_OK;
 }

@@ -1,0 +1,32 @@
+// zg_batch.h -- declarations shared by the batch kernels (zg_kernels.h) and the decode kernel
+// (zg_decode.h, its own translation unit): the batch buffer table and per-kind constants.
+#pragma once
+#include "zg_coop.h"
+#include "zg_groth16.h"
+#include "zg_prog.h"
+
+namespace zg {
+
+#define ZG_MSM_SLOTS (ZG_MAX_IC + 1)  // ic terms + the alpha term
+#define ZG_NPAIRS 3                   // per kind: (acc,-gamma) (C,-delta) (-S alpha, beta)
+
+__device__ __constant__ const int KIND_NINPUTS[ZG_NKINDS] = {7, 5, 9};
+
+struct BatchBufs {
+  const DevVK* vks;
+  const uint8_t* proofs;   // n x 192
+  const uint8_t* kinds;    // n
+  const uint8_t* inputs;   // n x 288
+  const uint8_t* ninputs;  // n or null
+  const uint8_t* r;        // n x 16
+  uint8_t* status;         // n
+  G1A* ptA;                // npad: r_i A_i (affine)
+  G2A* ptB;                // npad: B_i
+  Fq12* ftree;             // 2 npad
+  G1J* ctree;              // 2 npad x 3 kinds
+  Fr* stree;               // 2 npad x 3 kinds x ZG_MAX_IC (Montgomery)
+  int* bfail;              // count of B_i failing the (deferred) G2 subgroup check
+  int n, npad;
+};
+
+}  // namespace zg

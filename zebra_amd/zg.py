@@ -57,6 +57,7 @@ def lib():
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
         L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
         L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.zg_chacha20_blocks.argtypes = [vp, u8p, u8p, ctypes.c_uint32, ctypes.c_size_t, u8p]
         L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
         L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
         L.zg_prep_joinsplit.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
@@ -238,6 +239,13 @@ class Context:
         self._chk(lib().zg_synth_rerandomize(self._p, len(src_kinds), bytes(src_proofs), bytes(src_kinds), n, idx,
                                              seed, out))
         return out.raw[:192 * n]
+
+    def chacha20_blocks(self, key, nonce, counter, nblocks):
+        """the device ChaCha20 keystream (the batch-scalar CSPRNG), nblocks x 64 bytes"""
+        assert len(key) == 32 and len(nonce) == 12
+        out = ctypes.create_string_buffer(64 * max(nblocks, 1))
+        self._chk(lib().zg_chacha20_blocks(self._p, bytes(key), bytes(nonce), counter, nblocks, out))
+        return out.raw[:64 * nblocks]
 
     def bench_mad_rate(self):
         v = ctypes.c_double(0)
