@@ -405,12 +405,15 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 namespace zg {  // zg_decode.hip
 hipError_t launch_batch_decode(int w, unsigned groups, hipStream_t st, const BatchBufs& b);
 }
-static int decode_waves() {
-  static const int w = [] {
+// one wave per 64 proofs (all three chains) once that fills every SIMD (64k proofs); below,
+// one wave per chain for latency. ZG_DECODE_W=1|3 forces a variant (measurements).
+static int decode_waves(unsigned groups) {
+  static const int forced = [] {
     const char* e = getenv("ZG_DECODE_W");
-    return e && atoi(e) == 3 ? 3 : 1;
+    return e ? atoi(e) : 0;
   }();
-  return w;
+  if (forced == 1 || forced == 3) return forced;
+  return groups >= 1024 ? 1 : 3;
 }
 
 // The pipeline on device-resident inputs already in ctx buffers.
@@ -426,9 +429,8 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemsetAsync(b.bfail, 0, sizeof(int), ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  // one wave per chain (A, B, C) of 64 proofs, two waves per SIMD (zg_decode.hip)
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
-  HIPCHK(launch_batch_decode(decode_waves(), dgroups, ctx->stream, b));
+  HIPCHK(launch_batch_decode(decode_waves(dgroups), dgroups, ctx->stream, b));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   // side stream
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
