@@ -204,7 +204,7 @@ def main():
 
     total = shard * world
     value = total * args.steps / dt
-    names = ["k_batch_decode", "k_batch_lines", "k_batch_fchain", "k_tree_f", "root_partial", "side_stream_vk",
+    names = ["k_decode_points", "k_batch_lines", "k_batch_fchain", "k_tree_f", "root_partial", "side_stream_vk",
              "device_pipeline"]
     avg = [sum(t[i] for t in timings) / len(timings) for i in range(7)]
     dom = max(range(3), key=lambda i: avg[i])

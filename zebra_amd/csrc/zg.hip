@@ -41,7 +41,7 @@ struct zg_ctx {
   int* d_int = nullptr;  // scratch ints
   // batch
   uint8_t *d_proofs = nullptr, *d_kinds = nullptr, *d_inputs = nullptr, *d_ninputs = nullptr, *d_r = nullptr,
-          *d_status = nullptr, *d_bytes = nullptr;
+          *d_status = nullptr, *d_bytes = nullptr, *d_okbits = nullptr;
   G1A* d_ptA = nullptr;
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
@@ -105,6 +105,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
        dalloc(&ctx->d_inputs, (size_t)cap * 288) == hipSuccess && dalloc(&ctx->d_ninputs, cap) == hipSuccess &&
        dalloc(&ctx->d_r, ((size_t)cap + 3) / 4 * 64)  /* whole ChaCha20 blocks */ == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
+       dalloc(&ctx->d_okbits, (size_t)cap * 3) == hipSuccess &&
        dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
   ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
        dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
@@ -129,7 +130,8 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   hipSetDevice(ctx->device);
   void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
-                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines};
+                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
+                  ctx->d_okbits};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -387,6 +389,7 @@ static BatchBufs batch_bufs(zg_ctx* ctx) {
   b.ctree = ctx->d_ctree;
   b.stree = ctx->d_stree;
   b.bfail = ctx->d_int + 8;
+  b.okbits = ctx->d_okbits;
   b.n = (int)ctx->n;
   b.npad = (int)ctx->npad;
   return b;
@@ -403,17 +406,7 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 }
 
 namespace zg {  // zg_decode.hip
-hipError_t launch_batch_decode(int w, unsigned groups, hipStream_t st, const BatchBufs& b);
-}
-// one wave per 64 proofs (all three chains) once that fills every SIMD (64k proofs); below,
-// one wave per chain for latency. ZG_DECODE_W=1|3 forces a variant (measurements).
-static int decode_waves(unsigned groups) {
-  static const int forced = [] {
-    const char* e = getenv("ZG_DECODE_W");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 1 || forced == 3) return forced;
-  return groups >= 1024 ? 1 : 3;
+hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);
 }
 
 // The pipeline on device-resident inputs already in ctx buffers.
@@ -430,7 +423,7 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipMemsetAsync(b.bfail, 0, sizeof(int), ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
-  HIPCHK(launch_batch_decode(decode_waves(dgroups), dgroups, ctx->stream, b));
+  HIPCHK(launch_batch_decode(dgroups, ctx->stream, b));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   // side stream
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));

@@ -26,6 +26,7 @@ struct BatchBufs {
   G1J* ctree;              // 2 npad x 3 kinds
   Fr* stree;               // 2 npad x 3 kinds x ZG_MAX_IC (Montgomery)
   int* bfail;              // count of B_i failing the (deferred) G2 subgroup check
+  uint8_t* okbits;         // npad x {A, C, B}: the point decoded (k_decode_points -> k_decode_finish)
   int n, npad;
 };
 

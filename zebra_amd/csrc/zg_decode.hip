@@ -10,12 +10,10 @@
 
 namespace zg {
 
-// W = 1: one wave per 64 proofs runs the A, B and C chains; W = 3: one wave per chain.
-hipError_t launch_batch_decode(int w, unsigned groups, hipStream_t st, const BatchBufs& b) {
-  if (w == 1)
-    hipLaunchKernelGGL(k_batch_decode<1>, dim3(groups), dim3(64), 0, st, b);
-  else
-    hipLaunchKernelGGL(k_batch_decode<3>, dim3(groups), dim3(192), 0, st, b);
+// points (A, C, B waves), then per-proof statuses and leaves
+hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b) {
+  hipLaunchKernelGGL(k_decode_points, dim3(3 * groups), dim3(64), 0, st, b);
+  hipLaunchKernelGGL(k_decode_finish, dim3(groups), dim3(64), 0, st, b);
   return hipGetLastError();
 }
 
