@@ -205,9 +205,44 @@ def prog_m():
     return p, m014(p, ins[0:6], ins[6], ins[7], ins[8])
 
 
+def prog_mmsq():
+    """two-proof f-chain step: f = (f * line_0 * line_1)^2, the squaring shared by the pair of
+    proofs of one lane (their Miller values multiply into one product-tree node).
+    in: F0..F5 A B C (proof 2j) A2 B2 C2 (proof 2j+1)."""
+    p = Prog("mmsq", ["F0", "F1", "F2", "F3", "F4", "F5", "A", "B", "C", "A2", "B2", "C2"])
+    ins = [p.inp(i) for i in range(12)]
+    f1 = m014(p, ins[0:6], ins[6], ins[7], ins[8])
+    return p, f12_sqr(p, m014(p, f1, ins[9], ins[10], ins[11]))
+
+
+def prog_mm():
+    """two-proof f-chain step without the squaring: f = f * line_0 * line_1."""
+    p = Prog("mm", ["F0", "F1", "F2", "F3", "F4", "F5", "A", "B", "C", "A2", "B2", "C2"])
+    ins = [p.inp(i) for i in range(12)]
+    f1 = m014(p, ins[0:6], ins[6], ins[7], ins[8])
+    return p, m014(p, f1, ins[9], ins[10], ins[11])
+
+
 # ---------------------------------------------------------------- scheduling + slots
-def schedule(prog, outs, nw):
-    """list-schedule products into rounds of <= nw; allocate LDS slots with reuse."""
+def schedule(prog, outs, nw, search=0, max_slots=None):
+    """list-schedule products into rounds of <= nw; allocate LDS slots with reuse.
+    search > 0: also try that many seeded random tie-breaks among ready products and keep the
+    schedule with the fewest rounds whose slots fit max_slots (then the fewest slots)."""
+    best = _schedule(prog, outs, nw, None, 0)
+    if search:
+        rng = random.Random(20260101)
+        for t in range(search):
+            cand = _schedule(prog, outs, nw, rng, rng.choice([0.5, 1.5, 3, 6]))
+            fits = max_slots is None or cand["nslots"] <= max_slots
+            bfits = max_slots is None or best["nslots"] <= max_slots
+            key = (not fits, len(cand["rounds"]), cand["nslots"])
+            bkey = (not bfits, len(best["rounds"]), best["nslots"])
+            if key < bkey:
+                best = cand
+    return best
+
+
+def _schedule(prog, outs, nw, rng, slack):
     n = len(prog.prods)
     deps = []
     for L, R, _ in prog.prods:
@@ -224,7 +259,7 @@ def schedule(prog, outs, nw):
     done = set()
     while len(done) < n:
         ready = [i for i in range(n) if rnd[i] is None and all(j in done for j in deps[i])]
-        ready.sort(key=lambda i: (-height[i], i))
+        ready.sort(key=lambda i: (-height[i] + (rng.random() * slack if rng else 0), i))
         pick = ready[:nw]
         for i in pick:
             rnd[i] = len(rounds)
@@ -381,7 +416,7 @@ def emit(specs):
     out.append("__device__ __constant__ const int8_t PROG_SCHED[%d] = {%s};" % (len(sched), ", ".join(
         map(str, sched))))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
     out.append("// operands of global product gk; returns the product kind (f2_mul_kind)")
     out.append("__device__ __forceinline__ int prog_operands(int gk, const AtomSpace& at, Fq2& x, Fq2& y, int& dst) {")
@@ -406,9 +441,11 @@ NW_FCHAIN = 8
 
 def build_all():
     specs = []
-    for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN)):
+    for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
+                   (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN)):
         prog, outs = fn()
-        sch = schedule(prog, outs, nw)
+        # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
+        sch = schedule(prog, outs, nw, 3000, 25) if fn in (prog_mmsq, prog_mm) else schedule(prog, outs, nw)
         specs.append((prog.name, prog, outs, nw, sch))
     return specs
 

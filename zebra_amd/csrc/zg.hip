@@ -92,7 +92,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (!cfg) cfg = &def;
   ctx->device = cfg->device;
   uint32_t mb = cfg->max_batch ? cfg->max_batch : 65536;
-  uint32_t cap = 1;
+  uint32_t cap = 2;
   while (cap < mb) cap <<= 1;
   ctx->cap = cap;
   ctx->seeded = cfg->seeded;
@@ -441,10 +441,12 @@ static int run_pipeline(zg_ctx* ctx) {
   hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
-  hipLaunchKernelGGL(k_batch_fchain, dim3(groups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines);
+  // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
+  const unsigned pgroups = (unsigned)((ctx->npad / 2 + 63) / 64);
+  hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
+  for (size_t lo = ctx->npad / 4; lo >= 1; lo /= 2) {
     if (lo >= ZG_TREE_COOP_BELOW)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
@@ -477,7 +479,7 @@ static int begin_common(zg_ctx* ctx, size_t n) {
   if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
   ctx->root_pairs_ready = 0;
   ctx->n = n;
-  size_t npad = 1;
+  size_t npad = 2;  // at least one proof pair (the f-chain's unit)
   while (npad < n) npad <<= 1;
   ctx->npad = npad;
   ctx->calls++;
@@ -551,6 +553,14 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
       HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
       int rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream);
       if (rc) return rc;
+      // per-proof Miller leaves exist only on demand (the f-chain writes pair nodes)
+      bool leaves = false;
+      for (int q = 0; q < m; q++) leaves = leaves || nodes[off + q] >= (int)ctx->npad;
+      if (leaves) {
+        hipLaunchKernelGGL(k_leaf_miller, dim3(nblocks(m)), dim3(ZG_BLOCK), 0, ctx->stream, b, (const int*)ctx->d_nodes,
+                           m);
+        HIPCHK(hipGetLastError());
+      }
     }
     hipLaunchKernelGGL(k_node_final, dim3(m), dim3(64), 0, ctx->stream, b, nb, mode);
     HIPCHK(hipGetLastError());

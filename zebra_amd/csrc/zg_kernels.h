@@ -13,15 +13,6 @@
 
 namespace zg {
 
-// K6 (per proof): f_i = ML(r_i A_i, B_i) -> ftree leaf
-__global__ void __launch_bounds__(64) k_batch_miller(BatchBufs b) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= b.npad) return;
-  Fq12 f = f12_one();
-  if (i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf) f = miller_loop_1(b.ptA[i], b.ptB[i]);
-  b.ftree[b.npad + i] = f;
-}
-
 // ---------------------------------------------------------------------------------------
 // Per-proof Miller loop as two staged programs (zg_prog.h; lane = proof, wave = product):
 //   k_batch_lines : the R-chain (pairing's G2Prepared steps for B_i, with the ell scaling
@@ -111,26 +102,43 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
   }
 }
 
+// Two proofs per lane: the pair (2j, 2j+1) shares one Miller accumulator, f <- (f l_2j l_2j+1)^2
+// per step, so each step's Fq12 squaring serves both proofs (38 Fq2 products per pair-step
+// instead of 2 x 25). Their Miller values only ever meet as a product in the tree, whose node
+// npad/2 + j is exactly this pair: the f-chain writes that level directly. Per-proof leaves
+// (bisection below a failing pair) come from k_leaf_miller.
 // LDS slots: 0..5 f (Fq2 coefficients c0.c0 c0.c1 c0.c2 c1.c0 c1.c1 c1.c2), 6..8 the line A B C
+// of proof 2j, 9..11 of proof 2j+1. A proof that is not active contributes the line 1 (A = 1,
+// B = C = 0: f * (A + B v + C v w) = f).
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   const AtomSpace at{lds_atoms};
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
-  const int proof = blockIdx.x * 64 + lane;
-  const bool inb = proof < b.npad;
-  static_assert(ZG_FC_NW >= 7, "waves 0..5 carry f, waves 6.. load the line");
-  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
-  for (int j = wave - 6; j >= 0 && j < 3; j += ZG_FC_NW - 6)
-    at.put(6 + j, inb ? lines[(size_t)proof * 3 + j] : f2_one());
+  const int pair = blockIdx.x * 64 + lane;
+  const bool inb = pair < b.npad / 2;
+  const bool act0 = inb && proof_active(b, 2 * pair), act1 = inb && proof_active(b, 2 * pair + 1);
+  static_assert(ZG_FC_NW == 8, "waves 0..5 carry f, waves 6, 7 load the two lines");
+  // the pair's two line triples are adjacent in [step][proof][3]
+  auto load_lines = [&](int n) {
+    const Fq2* src = lines + ((size_t)n * b.npad + 2 * (size_t)pair) * 3;
+    for (int j = wave - 6; j < 6; j += 2) {
+      const bool act = j < 3 ? act0 : act1;
+      at.put(6 + j, act ? src[j] : (j % 3 == 0 ? f2_one() : f2_zero()));
+    }
+  };
+  if (wave < 6)
+    at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  else
+    load_lines(0);
   __syncthreads();
-  // per bit i (MSB first): [f *= dbl line; f = (f * add line)^2] or f = (f * dbl line)^2;
-  // then the last dbl line: f *= line
+  // per bit i (MSB first): [f *= dbl lines; f = (f * add lines)^2] or f = (f * dbl lines)^2;
+  // then the last dbl lines: f *= lines
   int n = 0;
   for (int i = ZG_XH_TOP;; i--) {
     const bool last = i < 0;
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
-      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_MM : ZG_PROG_MMSQ);
       prog_run(pid, at);
       Fq2 v;
       if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
@@ -139,19 +147,30 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, con
       if (wave < 6)
         at.put(wave, v);
       else if (n < ZG_NCOEFF)
-        for (int j = wave - 6; j < 3; j += ZG_FC_NW - 6)
-          at.put(6 + j, inb ? lines[((size_t)n * b.npad + proof) * 3 + j] : f2_one());
+        load_lines(n);
       __syncthreads();
     }
     if (last) break;
   }
-  // conjugate (u < 0) and store the leaf; inactive / padding proofs contribute 1
+  // conjugate (u < 0) and store the pair node
   if (wave < 6 && inb) {
     Fq2 v = at.get(wave);
     if (wave >= 3) v = f2_neg(v);
-    if (!proof_active(b, proof)) v = wave == 0 ? f2_one() : f2_zero();
-    reinterpret_cast<Fq2*>(&b.ftree[b.npad + proof])[wave] = v;
+    reinterpret_cast<Fq2*>(&b.ftree[b.npad / 2 + pair])[wave] = v;
   }
+}
+
+// Per-proof Miller leaves ftree[npad + i] for the listed leaf nodes (bisection below a failing
+// pair node; other nodes are skipped): pairing's miller_loop of (r_i A_i, B_i), 1 if inactive.
+__global__ void __launch_bounds__(64) k_leaf_miller(BatchBufs b, const int* nodes, int m) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= m) return;
+  const int node = nodes[q];
+  if (node < b.npad) return;
+  const int i = node - b.npad;
+  Fq12 f = f12_one();
+  if (proof_active(b, i)) f = miller_loop_1(b.ptA[i], b.ptB[i]);
+  b.ftree[node] = f;
 }
 
 // Fq12 product-tree level: nodes [lo, 2 lo)
