@@ -27,6 +27,14 @@ __global__ void __launch_bounds__(64) k_bench(const Fq12* in, Fq12* out, long lo
   __syncthreads();
   for (int i = 0; i < iters; i++) coop_copy(&ws, 3, 2);
   long long t6 = clock64();
+  coop_load(&ws, 4, in[0]);
+  coop_csqr(&ws, 5, 4);
+  coop_csqr1(&ws, 6, 4);
+  int diff = 0;
+  for (int k = 0; k < 12; k++) diff |= !fq_eq(ws.slot[5][k], ws.slot[6][k]);
+  long long t7 = clock64();
+  for (int i = 0; i < iters; i++) coop_csqr1(&ws, 4, 4);
+  long long t8 = clock64();
   coop_store(&ws, 0, out[0]);
   coop_store(&ws, 2, out[1]);
   if (threadIdx.x == 0) {
@@ -36,6 +44,8 @@ __global__ void __launch_bounds__(64) k_bench(const Fq12* in, Fq12* out, long lo
     cyc[3] = t4 - t3;
     cyc[4] = t5 - t4;
     cyc[5] = t6 - t5;
+    cyc[6] = t8 - t7;
+    cyc[7] = diff;
   }
 }
 
@@ -67,9 +77,10 @@ int main() {
     hipDeviceSynchronize();
   }
   long long c[8];
-  hipMemcpy(c, dc, 48, hipMemcpyDeviceToHost);
   const char* names[] = {"csqr", "mul", "sqr", "mul014", "fq_mul (1 lane chain)", "copy"};
+  hipMemcpy(c, dc, 64, hipMemcpyDeviceToHost);
   for (int i = 0; i < 6; i++) printf("%-22s %8.0f cycles/op\n", names[i], (double)c[i] / iters);
+  printf("%-22s %8.0f cycles/op  (equals coop_csqr: %s)\n", "csqr1", (double)c[6] / iters, c[7] ? "NO" : "yes");
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);

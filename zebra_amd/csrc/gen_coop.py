@@ -39,8 +39,9 @@ class Lin(dict):
 
 
 class Op:
-    def __init__(self, name):
+    def __init__(self, name, flat=False):
         self.name = name
+        self.flat = flat  # flat: no intermediate sums, outputs are forms of products and inputs
         self.atoms = []  # (kind, level, forms): kind 'p' (L, R) or 's' (form,)
 
     def level_of(self, f):
@@ -57,7 +58,7 @@ class Op:
 
     def mat(self, f):
         """materialise a form as a sum atom (one lane task)"""
-        if len(f) == 1 and list(f.values())[0] == 1:
+        if self.flat or len(f) == 1 and list(f.values())[0] == 1:
             return f
         self.atoms.append(("s", 1 + max(0, self.level_of(f)), (f,)))
         return Lin({NIN + len(self.atoms) - 1: 1})
@@ -191,8 +192,8 @@ def flat(x):
     return [v for h in x for c in h for v in c]
 
 
-def build(name, fn):
-    op = Op(name)
+def build(name, fn, flat_forms=False):
+    op = Op(name, flat_forms)
     out = flat(fn(op, sym(0), sym(12)))
     # levels: products 0, sums by dependency, outputs last
     nlev = 1 + max([a[1] for a in op.atoms] + [0])
@@ -280,6 +281,8 @@ def check(ops):
             elif op["name"] == "m014":
                 bs = [b[0], b[1], b[2], b[3], 0, 0, 0, 0, b[8], b[9], 0, 0]
                 want = flat(rf12_mul(unflat(a), unflat(bs)))
+            elif op["name"] == "csqr1":
+                want = evaluate([o for o in ops if o["name"] == "csqr"][0], a, b)  # same map, one level
             else:
                 continue  # csqr: valid only on cyclotomic elements (checked on the device path)
             assert got == want, op["name"]
@@ -336,9 +339,29 @@ def emit(ops):
     return lines
 
 
+def check_csqr1_products(op):
+    """coop_csqr1 computes the product operands in code, not from these forms: product
+    k = 6 p + 2 w + h squares x = z_a (w 0), z_b (w 1) or z_a + z_b (w 2) of the Fp4 pair p,
+    with operands (x0, x1) for h = 0 and (x0 + x1, x0 - x1) for h = 1; the pairs' Fq2
+    coefficient indices are (0, 4), (3, 2), (1, 5)."""
+    pairs = [(0, 4), (3, 2), (1, 5)]
+    (prods,) = op["levels"]
+    assert len(prods) == 18
+    for k, (L, R) in enumerate(prods):
+        p, w, h = k // 6, (k % 6) // 2, k % 2
+        ja, jb = pairs[p]
+        sel = [ja] if w == 0 else [jb] if w == 1 else [ja, jb]
+        x0 = Lin({2 * j: 1 for j in sel})
+        x1 = Lin({2 * j + 1: 1 for j in sel})
+        want = (x0, x1) if h == 0 else (x0 + x1, x0 - x1)
+        assert (dict(L), dict(R)) == (dict(want[0]), dict(want[1])), k
+
+
 def main():
-    ops = [build("mul", f12_mul), build("sqr", f12_sqr), build("csqr", f12_cyc_sqr), build("m014", f12_mul_014)]
+    ops = [build("mul", f12_mul), build("sqr", f12_sqr), build("csqr", f12_cyc_sqr), build("m014", f12_mul_014),
+           build("csqr1", f12_cyc_sqr, flat_forms=True)]
     check(ops)
+    check_csqr1_products(ops[-1])
     sys.stdout.write("\n".join(emit(ops)) + "\n")
     for o in ops:
         sys.stderr.write("%s: levels %s, max terms %d\n" % (

@@ -16,11 +16,39 @@
 namespace zg {
 
 #define ZG_COOP_SLOTS 8
-struct CoopWS {
+// LDS copy of a form: up to 8 terms packed from t[0], a zero term ends the list (a real term
+// has a nonzero coefficient); 16 B so that one ds_read_b128 fetches the whole form.
+struct alignas(16) CoopFormL {
+  int16_t t[ZG_COOP_MAXT];
+};
+struct alignas(16) CoopWS {
   Fq slot[ZG_COOP_SLOTS][12];       // Fq12 registers, coefficient order of f12_coeffs
   Fq v[24 + ZG_COOP_MAXATOMS];      // op workspace: inputs a (0..11), b (12..23), then atoms
-  CoopForm forms[ZG_COOP_NFORMS];   // LDS copy of COOP_FORMS (per-lane table reads at LDS latency)
+  CoopFormL forms[ZG_COOP_NFORMS];  // LDS copy of COOP_FORMS (per-lane table reads at LDS latency)
 };
+static_assert(sizeof(Fq) == 48 && offsetof(CoopWS, v) % 16 == 0 && offsetof(CoopWS, forms) % 16 == 0, "LDS layout");
+// The workspace always lives in LDS; kernels hand it around as a generic pointer, so the hot
+// paths re-qualify it once (LDS instructions instead of flat ones with null checks).
+#define ZG_LDS __attribute__((address_space(3)))
+typedef ZG_LDS CoopWS LdsWS;
+ZG_INL LdsWS* lds_ws(CoopWS* ws) { return (LdsWS*)ws; }
+ZG_INL void lds_get(const ZG_LDS Fq* p, u32x4& a, u32x4& b, u32x4& c) {
+  const ZG_LDS u32x4* q = (const ZG_LDS u32x4*)p;
+  a = q[0];
+  b = q[1];
+  c = q[2];
+}
+ZG_INL Fq lds_fq(const ZG_LDS Fq* p) {
+  u32x4 a, b, c;
+  lds_get(p, a, b, c);
+  return {{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w}};
+}
+ZG_INL void lds_put(ZG_LDS Fq* p, const Fq& x) {
+  ZG_LDS u32x4* q = (ZG_LDS u32x4*)p;
+  q[0] = u32x4{x.l[0], x.l[1], x.l[2], x.l[3]};
+  q[1] = u32x4{x.l[4], x.l[5], x.l[6], x.l[7]};
+  q[2] = u32x4{x.l[8], x.l[9], x.l[10], x.l[11]};
+}
 
 // Lazy linear forms  sum_t c_t x_t  (|c_t| < 128, <= 8 terms, x_t any 384-bit value):
 // one 64-bit accumulator per limb, no carry chain per term. A negative term adds
@@ -79,36 +107,49 @@ ZG_INL Fq lazy_finish(const LazyAcc& a, bool canon) {
   return r;
 }
 
-__device__ __forceinline__ Fq coop_form(const CoopWS* ws, int fi, bool canon) {
-  const CoopForm& f = ws->forms[fi];
+ZG_INL void lazy_term4(LazyAcc& a, const u32x4& x0, const u32x4& x1, const u32x4& x2, int c) {
+  const Fq x = {{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w}};
+  lazy_term(a, x, c);
+}
+
+// One linear form: the descriptor in one LDS read, then its terms two at a time with both
+// operands' loads in flight together (a zero coefficient adds nothing).
+ZG_INL Fq coop_form(const LdsWS* ws, int fi, bool canon) {
+  const u32x4 d = *(const ZG_LDS u32x4*)&ws->forms[fi];
+  const uint32_t w[4] = {d.x, d.y, d.z, d.w};
   LazyAcc acc;
   lazy_zero(acc);
-  const int n = f.n;
-  for (int q = 0; q < n; q++) {
-    const int v = f.t[q];
-    lazy_term(acc, ws->v[v & 0xff], v >> 8);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int t0 = (int)(int16_t)(w[q] & 0xffffu), t1 = (int)(int16_t)(w[q] >> 16);
+    if (t0 == 0) break;
+    u32x4 a0, a1, a2, b0, b1, b2;
+    lds_get(&ws->v[t0 & 0xff], a0, a1, a2);
+    lds_get(&ws->v[t1 & 0xff], b0, b1, b2);
+    lazy_term4(acc, a0, a1, a2, t0 >> 8);
+    lazy_term4(acc, b0, b1, b2, t1 >> 8);
   }
   return lazy_finish(acc, canon);
 }
 
 // copy the form tables into the block's LDS (once per kernel, before any coop op)
-__device__ void coop_init(CoopWS* ws) {
-  const uint16_t* src = reinterpret_cast<const uint16_t*>(COOP_FORMS);
-  uint16_t* dst = reinterpret_cast<uint16_t*>(ws->forms);
-  constexpr int nw = (int)(sizeof(CoopForm) * ZG_COOP_NFORMS / 2);
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+__device__ void coop_init(CoopWS* ws_g) {
+  LdsWS* ws = lds_ws(ws_g);
+  for (int i = threadIdx.x; i < ZG_COOP_NFORMS * ZG_COOP_MAXT; i += blockDim.x) {
+    const CoopForm& f = COOP_FORMS[i / ZG_COOP_MAXT];
+    const int q = i % ZG_COOP_MAXT;
+    ws->forms[i / ZG_COOP_MAXT].t[q] = q < f.n ? f.t[q] : (int16_t)0;
+  }
   __syncthreads();
 }
 
 // slot[dst] = op(slot[a], slot[b]) for op = ZG_COOP_{MUL,SQR,CSQR,M014}; dst may alias a / b.
 // Level 0: one Fq product per lane; later levels: one linear form per lane; the last level
 // writes the 12 output coefficients.
-__device__ void coop_run(CoopWS* ws, int opid, int dst, int a, int b) {
+__device__ void coop_run(CoopWS* ws_g, int opid, int dst, int a, int b) {
+  LdsWS* ws = lds_ws(ws_g);
   const int lane = threadIdx.x & 63;
-  if (lane < 12) {
-    ws->v[lane] = ws->slot[a][lane];
-    ws->v[12 + lane] = ws->slot[b][lane];
-  }
+  if (lane < 24) lds_put(&ws->v[lane], lds_fq(&ws->slot[lane < 12 ? a : b][lane < 12 ? lane : lane - 12]));
   __syncthreads();
   const CoopOp& op = COOP_OPS[opid];
   const int nlev = op.nlev;
@@ -118,18 +159,70 @@ __device__ void coop_run(CoopWS* ws, int opid, int dst, int a, int b) {
     if (lane < cnt) {
       if (l == 0) {
         const Fq x = coop_form(ws, off + 2 * lane, false), y = coop_form(ws, off + 2 * lane + 1, false);
-        ws->v[base + lane] = fq_mul(x, y);
+        lds_put(&ws->v[base + lane], fq_mul(x, y));
       } else {
         const Fq x = coop_form(ws, off + lane, l == nlev - 1);
-        if (l == nlev - 1)
-          ws->slot[dst][lane] = x;
-        else
-          ws->v[base + lane] = x;
+        lds_put(l == nlev - 1 ? &ws->slot[dst][lane] : &ws->v[base + lane], x);
       }
     }
     base += cnt;
     __syncthreads();
   }
+}
+
+// 384-bit a + b and a + p - b without reduction (a, b < p: results < 2p, valid fq_mul operands)
+ZG_INL Fq raw_add(const Fq& a, const Fq& b) {
+  Fq r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    c += (uint64_t)a.l[i] + b.l[i];
+    r.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return r;
+}
+ZG_INL Fq raw_sub_p(const Fq& a, const Fq& b) {
+  Fq r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    c += (int64_t)a.l[i] + FQ_P[i] - b.l[i];
+    r.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return r;
+}
+
+// Granger-Scott squaring (cyclotomic subgroup only) in ONE product level: lane k < 18 squares
+// a coefficient of an Fp4 pair with its operands formed in code (gen_coop.py
+// check_csqr1_products pins the mapping), then 12 lanes evaluate the output forms of ZG_COOP_CSQR1
+// (products and inputs, <= 4 terms). Same value as coop_csqr; about half its latency.
+__device__ void coop_csqr1(CoopWS* ws_g, int dst, int a) {
+  LdsWS* ws = lds_ws(ws_g);
+  const int lane = threadIdx.x & 63;
+  if (lane < 12) lds_put(&ws->v[lane], lds_fq(&ws->slot[a][lane]));
+  __syncthreads();
+  if (lane < 18) {
+    const int p = lane / 6, w = (lane % 6) >> 1, h = lane & 1;
+    const int ja = p == 0 ? 0 : p == 1 ? 3 : 1, jb = p == 0 ? 4 : p == 1 ? 2 : 5;
+    const int j = w == 1 ? jb : ja;
+    Fq x0 = lds_fq(&ws->v[2 * j]), x1 = lds_fq(&ws->v[2 * j + 1]);
+    if (w == 2) {
+      x0 = fq_add(x0, lds_fq(&ws->v[2 * jb]));
+      x1 = fq_add(x1, lds_fq(&ws->v[2 * jb + 1]));
+    }
+    Fq l = x0, r = x1;
+    if (h) {
+      l = raw_add(x0, x1);
+      r = raw_sub_p(x0, x1);
+    }
+    lds_put(&ws->v[24 + lane], fq_mul(l, r));
+  }
+  __syncthreads();
+  const CoopOp& op = COOP_OPS[ZG_COOP_CSQR1];
+  if (lane < 12) lds_put(&ws->slot[dst][lane], coop_form(ws, op.off[1] + lane, true));
+  __syncthreads();
 }
 
 __device__ __forceinline__ void coop_mul(CoopWS* ws, int dst, int a, int b) { coop_run(ws, ZG_COOP_MUL, dst, a, b); }
@@ -212,7 +305,7 @@ __device__ void coop_exp_by_x(CoopWS* ws, int dst, int a, uint64_t x, int tmp) {
   int top = 63;
   while (!((x >> top) & 1ull)) top--;
   for (int i = top - 1; i >= 0; i--) {
-    coop_csqr(ws, tmp, tmp);
+    coop_csqr1(ws, tmp, tmp);
     if ((x >> i) & 1ull) coop_mul(ws, tmp, tmp, a);
   }
   coop_conj(ws, dst, tmp);
@@ -230,7 +323,7 @@ __device__ void coop_final_exp(CoopWS* ws, int in, int out) {
   coop_frob(ws, Rr, Rr, 2);
   coop_mul(ws, Rr, Rr, F2);     // r = frob2(r) * f2
   const uint64_t x = BLS_X;
-  coop_csqr(ws, Y0, Rr);                 // y0 = r^2
+  coop_csqr1(ws, Y0, Rr);                // y0 = r^2
   coop_exp_by_x(ws, Y1, Y0, x, T);       // y1 = y0^x
   coop_exp_by_x(ws, Y2, Y1, x >> 1, T);  // y2 = y1^(x/2)
   coop_conj(ws, Y3, Rr);                 // y3 = conj(r)
