@@ -43,6 +43,7 @@ struct zg_ctx {
   uint8_t *d_proofs = nullptr, *d_kinds = nullptr, *d_inputs = nullptr, *d_ninputs = nullptr, *d_r = nullptr,
           *d_status = nullptr, *d_bytes = nullptr, *d_okbits = nullptr;
   G1A* d_ptA = nullptr;
+  G1A* d_ptAC = nullptr;
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
@@ -107,7 +108,8 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
        dalloc(&ctx->d_r, ((size_t)cap + 3) / 4 * 64)  /* whole ChaCha20 blocks */ == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
        dalloc(&ctx->d_okbits, (size_t)cap * 3) == hipSuccess &&
        dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
-  ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
+  ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess &&
+       dalloc(&ctx->d_ptAC, 2 * (size_t)cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
        dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
        dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3) == hipSuccess &&
        dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
@@ -131,7 +133,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
-                  ctx->d_okbits};
+                  ctx->d_okbits, ctx->d_ptAC};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -385,6 +387,7 @@ static BatchBufs batch_bufs(zg_ctx* ctx) {
   b.status = ctx->d_status;
   b.ptA = ctx->d_ptA;
   b.ptB = ctx->d_ptB;
+  b.ptAC = ctx->d_ptAC;
   b.ftree = ctx->d_ftree;
   b.ctree = ctx->d_ctree;
   b.stree = ctx->d_stree;

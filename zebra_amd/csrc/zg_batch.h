@@ -22,6 +22,7 @@ struct BatchBufs {
   uint8_t* status;         // n
   G1A* ptA;                // npad: r_i A_i (affine)
   G2A* ptB;                // npad: B_i
+  G1A* ptAC;               // 2 npad: A_i then C_i as decompressed (k_decode_sqrt -> k_decode_points)
   Fq12* ftree;             // 2 npad
   G1J* ctree;              // 2 npad x 3 kinds
   Fr* stree;               // 2 npad x 3 kinds x ZG_MAX_IC (Montgomery)

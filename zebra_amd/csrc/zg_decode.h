@@ -7,47 +7,67 @@
 
 namespace zg {
 
-// K1 + K2 + K3 as two launches.
+// K1 + K2 + K3 as three launches.
 //
-// k_decode_points: one wave per (64 proofs, point). Blocks [0, 2G) alternate A / C of the same
-// 64 proofs: Fq sqrt, G1 subgroup check and the GLV product [r_i] P (A: to affine -> ptA,
-// C: Jacobian -> the proof's ctree leaf of its kind); blocks [2G, 3G) decompress B (Fq2 sqrt;
-// its G2 subgroup check rides on k_batch_lines). The heavy G1 waves are dispatched first, two
-// per SIMD (ZG_DECODE_WPE), and the shorter B waves fill the tail. The scalar products run
-// before the statuses are known (a failed decode skips its own; the rest are masked below).
-// A 64k batch is 3072 waves: 3x the waves of one lane-per-proof kernel, at twice its issue rate
-// per SIMD.
+// k_decode_sqrt: one wave per (64 proofs, G1 point), blocks alternating A / C of the same 64
+// proofs: flags, x < p, Fq sqrt and the sign choice of G1Compressed::into_affine. The affine
+// point goes to ptAC (inf = the point did not decode).
+//
+// k_decode_points: one wave per (64 proofs, job), the jobs of a decoded point being independent
+// of each other: blocks [0, 2G) alternate the GLV products [r_i] A_i (to affine -> ptA) and
+// [r_i] C_i (Jacobian -> the proof's ctree leaf of its kind); blocks [2G, 4G) alternate the G1
+// subgroup checks of A and C (sigma(P) = -[x^2] P -> okbits); blocks [4G, 5G) decompress B (Fq2
+// sqrt; its G2 subgroup check rides on k_batch_lines). Splitting the subgroup check off the
+// scalar product takes ~40 % off the longest chain a wave runs, which is what a small shard
+// (an 8,192-proof rank of the 8-GPU run: 640 waves on 1,024 SIMDs) waits for; the total work
+// is unchanged. The heavy waves are dispatched first, two per SIMD (ZG_DECODE_WPE), and the B
+// waves fill the tail. The scalar products run before the statuses are known (a point that did
+// not decode skips its own; the rest are masked by k_decode_finish).
+__global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) {
+  const int role = blockIdx.x & 1;  // 0 A, 1 C (wave-uniform)
+  const int i = (blockIdx.x >> 1) * 64 + (threadIdx.x & 63);
+  if (i >= b.npad) return;
+  G1A p;
+  p.inf = true;
+  if (i < b.n && g1_decompress(b.proofs + (size_t)i * 192 + (role == 0 ? 0 : 144), &p, false) != DEC_OK)
+    p.inf = true;
+  b.ptAC[(size_t)role * b.npad + i] = p;
+}
+
 __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b) {
   const int G = (b.npad + 63) / 64;
   const int blk = blockIdx.x;
-  const int role = blk < 2 * G ? (blk & 1) : 2;  // 0 A, 1 C, 2 B (wave-uniform)
-  const int grp = blk < 2 * G ? (blk >> 1) : blk - 2 * G;
-  const int lane = threadIdx.x & 63;
-  const int i = grp * 64 + lane;
-  const bool inb = i < b.npad, live = i < b.n;
+  const int job = blk < 2 * G ? 0 : blk < 4 * G ? 1 : 2;  // 0 GLV, 1 subgroup, 2 B (wave-uniform)
+  const int role = job == 2 ? 2 : (blk & 1);             // 0 A, 1 C, 2 B
+  const int grp = job == 2 ? blk - 4 * G : (blk - 2 * G * job) >> 1;
+  const int i = grp * 64 + (threadIdx.x & 63);
+  if (i >= b.npad) return;
   const int leaf = b.npad + i;
-  bool ok = false;
-  if (role == 2) {
+  if (job == 2) {
     G2A q;
     q.inf = true;
-    if (live) ok = g2_decompress(b.proofs + (size_t)i * 192 + 48, &q, false) == DEC_OK;
-    if (inb) b.ptB[i] = q;
-  } else {
-    G1A p;
-    p.inf = true;
-    if (live) ok = g1_decompress(b.proofs + (size_t)i * 192 + (role == 0 ? 0 : 144), &p) == DEC_OK;
-    uint64_t ra = 0, rb = 0;
-    if (ok) batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
-    if (role == 0) {
-      G1A o;
-      o.inf = true;
-      if (ok) o = jac_to_aff(g1_glv_mul(p, ra, rb));
-      if (inb) b.ptA[i] = o;
-    } else if (ok) {
-      b.ctree[leaf * ZG_NKINDS + b.kinds[i]] = g1_glv_mul(p, ra, rb);
-    }
+    bool ok = false;
+    if (i < b.n) ok = g2_decompress(b.proofs + (size_t)i * 192 + 48, &q, false) == DEC_OK;
+    b.ptB[i] = q;
+    b.okbits[3 * i + 2] = ok;
+    return;
   }
-  if (inb) b.okbits[3 * i + role] = ok;
+  const G1A p = b.ptAC[(size_t)role * b.npad + i];
+  const bool ok = !p.inf;
+  if (job == 1) {
+    b.okbits[3 * i + role] = ok && g1_in_subgroup(p);
+    return;
+  }
+  uint64_t ra = 0, rb = 0;
+  if (ok) batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
+  if (role == 0) {
+    G1A o;
+    o.inf = true;
+    if (ok) o = jac_to_aff(g1_glv_mul(p, ra, rb));
+    b.ptA[i] = o;
+  } else if (ok) {
+    b.ctree[leaf * ZG_NKINDS + b.kinds[i]] = g1_glv_mul(p, ra, rb);
+  }
 }
 
 // k_decode_finish: lane = proof. bellman's precedence (sapling.rs:157-167): input canonicity,
