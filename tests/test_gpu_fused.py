@@ -1,0 +1,74 @@
+"""GPU tier: the two launch shapes of the R-chain + f-chain (zg_kernels.h k_lines_fchain vs
+k_batch_lines then k_batch_fchain), forced through ZG_LINES_FCHAIN (read by zg_create), give
+the same statuses, GT bytes and 576-byte Miller partials. The fused shape is the default for
+shards whose two grids fit on the device at once (the 8-GPU run's 8,192-proof ranks); forcing
+it on a 16,384-proof batch puts more blocks in flight than there are CUs."""
+import os
+
+import pytest
+
+from tests.conftest import load_golden
+from tests.test_gpu_parity import corrupted_4096, fx_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def make_ctx(mode, max_batch=16384):
+    from zebra_amd import Context
+    old = os.environ.get("ZG_LINES_FCHAIN")
+    os.environ["ZG_LINES_FCHAIN"] = mode
+    try:
+        return Context(device=0, max_batch=max_batch, seed=7)
+    finally:
+        if old is None:
+            del os.environ["ZG_LINES_FCHAIN"]
+        else:
+            os.environ["ZG_LINES_FCHAIN"] = old
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    cs = {m: make_ctx(m) for m in ("0", "1")}
+    yield cs
+    for c in cs.values():
+        c.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_batch64_statuses_and_gt(ctxs, mode):
+    b = load_golden("batch64.json")
+    items = b["items"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    r = b"".join(bytes.fromhex(e["r"]) for e in items)
+    sts, gt = ctxs[mode].verify_batch(proofs, kinds, inputs, nin, r=r, want_gt=True)
+    assert sts == [e["status"] for e in items]
+    assert gt.hex() == b["gt_out"]
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_corrupted_4096(ctxs, mode):
+    """non-subgroup B among them: the fused launch's gated f-chain re-run (bfail) path"""
+    proofs, kinds, inputs, want = corrupted_4096(ctxs[mode])
+    sts, _ = ctxs[mode].verify_batch(proofs, kinds, inputs)
+    assert sts == want
+
+
+@pytest.mark.parametrize("n", [128, 4096, 16384])
+def test_partials_equal(ctxs, n):
+    """same seeded r_i, same proofs: the two shapes produce the same Miller partial bytes"""
+    from zebra_amd import pack_inputs
+    real = load_golden("real_proofs.json")["proofs"]
+    src_proofs = b"".join(bytes.fromhex(e["proof"]) for e in real)
+    src_kinds = bytes(e["kind"] for e in real)
+    idx = [i % len(real) for i in range(n)]
+    proofs = ctxs["0"].synth_rerandomize(src_proofs, src_kinds, idx, 5)
+    kinds = bytes(src_kinds[j] for j in idx)
+    inputs = pack_inputs([[bytes.fromhex(x) for x in real[j]["inputs"]] for j in idx])
+    parts = []
+    for mode in ("0", "1"):
+        c = ctxs[mode]
+        c.batch_begin(proofs, kinds, inputs)
+        parts.append(c.batch_partial())
+        assert c.gt_check([parts[-1]])
+        assert c.batch_finish(True, n) == [0] * n
+    assert parts[0] == parts[1]

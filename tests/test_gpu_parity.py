@@ -124,6 +124,12 @@ def test_split_partials(ctx):
 
 def test_batch_4096_one_percent_corrupted(ctx):
     """config 4 shape: 4,096 re-randomized proofs, 41 corrupted -> exact reject set."""
+    proofs, kinds, inputs, want = corrupted_4096(ctx)
+    sts, _ = ctx.verify_batch(proofs, kinds, inputs)
+    assert sts == want
+
+
+def corrupted_4096(ctx):
     import random
     from zebra_amd import pack_inputs
     real = load_golden("real_proofs.json")["proofs"]
@@ -157,8 +163,7 @@ def test_batch_4096_one_percent_corrupted(ctx):
         else:             # non-subgroup G1 A -> DECODE_INVALID
             proofs[192 * i:192 * i + 48] = bytes.fromhex(pts["g1_not_in_subgroup"])
             want[i] = 1
-    sts, _ = ctx.verify_batch(bytes(proofs), bytes(src_kinds[j] for j in idx), pack_inputs(rows))
-    assert sts == want
+    return bytes(proofs), bytes(src_kinds[j] for j in idx), pack_inputs(rows), want
 
 
 def test_partial_bitexact_vs_oracle(ctx):

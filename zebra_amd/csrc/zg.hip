@@ -4,6 +4,7 @@
 // on the GPU; the host parses bytes, drives launches and the bisection, and moves data.
 #include <hip/hip_runtime.h>
 #include <errno.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
@@ -44,6 +45,9 @@ struct zg_ctx {
           *d_status = nullptr, *d_bytes = nullptr, *d_okbits = nullptr;
   G1A* d_ptA = nullptr;
   G1A* d_ptAC = nullptr;
+  int* d_prog = nullptr;  // cap / 64: per lines block, steps published (fused R-chain + f-chain)
+  int ncu = 0;            // compute units of the device
+  int fuse = -1;          // ZG_LINES_FCHAIN: -1 auto (both grids resident at once), 0 never, 1 always
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
@@ -101,6 +105,8 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   bool ok = hipSetDevice(ctx->device) == hipSuccess &&
             hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess;
+  if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   ok = ok && dalloc(&ctx->d_vk, ZG_NKINDS) == hipSuccess && dalloc(&ctx->d_rawvk, 1) == hipSuccess &&
        dalloc(&ctx->d_int, 16) == hipSuccess;
   ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
@@ -109,7 +115,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
        dalloc(&ctx->d_okbits, (size_t)cap * 3) == hipSuccess &&
        dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
   ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess &&
-       dalloc(&ctx->d_ptAC, 2 * (size_t)cap) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
+       dalloc(&ctx->d_ptAC, 2 * (size_t)cap) == hipSuccess && dalloc(&ctx->d_prog, (size_t)cap / 64 + 1) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
        dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
        dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3) == hipSuccess &&
        dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
@@ -133,7 +139,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
-                  ctx->d_okbits, ctx->d_ptAC};
+                  ctx->d_okbits, ctx->d_ptAC, ctx->d_prog};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -423,7 +429,7 @@ static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   static const int root = 1;
   HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemsetAsync(b.bfail, 0, sizeof(int), ctx->stream));
+  HIPCHK(hipMemsetAsync(b.bfail, 0, 2 * sizeof(int), ctx->stream));  // bfail, fused-wait failure
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
   HIPCHK(launch_batch_decode(dgroups, ctx->stream, b));
@@ -440,13 +446,25 @@ static int run_pipeline(zg_ctx* ctx) {
   if (rc) return rc;
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->side));
   // main stream: the R-chain (lines; also the G2 subgroup checks of the B_i), then the f-chain
-  const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
-  hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
   // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
+  const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
   const unsigned pgroups = (unsigned)((ctx->npad / 2 + 63) / 64);
-  hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b, ctx->d_lines);
+  const bool fused = ctx->fuse == 1 || (ctx->fuse < 0 && groups + pgroups <= (unsigned)ctx->ncu);
+  if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
+    HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
+    hipLaunchKernelGGL(k_lines_fchain, dim3(groups + pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
+                       ctx->d_lines, ctx->d_prog, b.bfail + 1);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
+                       (const Fq2*)ctx->d_lines, (const int*)b.bfail);  // no-op unless bfail / wait failure
+  } else {
+    hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+    hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
+                       (const Fq2*)ctx->d_lines, (const int*)nullptr);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   for (size_t lo = ctx->npad / 4; lo >= 1; lo /= 2) {

@@ -23,6 +23,7 @@ namespace zg {
 #define ZG_LINES_NW 6   // widest round of dbl/add
 #define ZG_FC_NW 8      // 2 waves per SIMD (256 VGPRs, no spills); msq = 4 rounds
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
+#define ZG_PUB_STEPS 4  // fused launch: lines steps per publish
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
   return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
@@ -33,11 +34,11 @@ __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
 // The R-chain of pairing's G2Prepared is the double-and-add of [x] B (x = |u|, Jacobian), so
 // the G2 subgroup check of B (psi(B) = [u] B, zg_curve.h) is its last step here: a B that
 // fails it turns its proof DECODE_INVALID (Proof::read) and its leaves back to the identity.
-__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines) {
-  __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
-  const AtomSpace at{lds_atoms};
+// prog (fused launch only): per lines block the number of steps whose triples are in HBM.
+__device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int blk, const AtomSpace& at,
+                                           int* prog) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
-  const int proof = blockIdx.x * 64 + lane;
+  const int proof = blk * 64 + lane;
   const bool act = proof_active(b, proof);
   const bool chk = proof < b.n && !b.ptB[proof].inf;  // B owes its subgroup check
   if (wave == 0) {
@@ -79,8 +80,12 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
         at.put(wave, v);
       else if (wave < 6 && proof < b.npad)
         lines[((size_t)n * b.npad + proof) * 3 + (wave - 3)] = act ? v : f2_one();
+      // publish every ZG_PUB_STEPS steps: each wave's stores released, then the count
+      const bool pub = prog && ((n + 1) % ZG_PUB_STEPS == 0 || n + 1 == ZG_NCOEFF);
+      if (pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __syncthreads();
       n++;
+      if (pub && threadIdx.x == 0) __hip_atomic_store(&prog[blk], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // R = [x] B (Jacobian). B in G2  <=>  psi(B) = [u] B = -[x] B  <=>  X = psi_x Z^2, Y = -psi_y Z^3,
@@ -101,6 +106,10 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
     }
   }
 }
+__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines) {
+  __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
+  lines_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr);
+}
 
 // Two proofs per lane: the pair (2j, 2j+1) shares one Miller accumulator, f <- (f l_2j l_2j+1)^2
 // per step, so each step's Fq12 squaring serves both proofs (38 Fq2 products per pair-step
@@ -110,16 +119,43 @@ __global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, F
 // LDS slots: 0..5 f (Fq2 coefficients c0.c0 c0.c1 c0.c2 c1.c0 c1.c1 c1.c2), 6..8 the line A B C
 // of proof 2j, 9..11 of proof 2j+1. A proof that is not active contributes the line 1 (A = 1,
 // B = C = 0: f * (A + B v + C v w) = f).
-__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines) {
-  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  const AtomSpace at{lds_atoms};
+// prog / fail (fused launch only): wait until both lines blocks of this block's 128 proofs have
+// published step n; a wait that outlasts ~0.5 s (the producers were not resident -- never
+// expected, see k_lines_fchain) sets *fail, stops waiting, and the gated k_batch_fchain after
+// the launch recomputes everything.
+__device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines, int blk, const AtomSpace& at,
+                                            const int* prog, int* fail) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
-  const int pair = blockIdx.x * 64 + lane;
+  const int pair = blk * 64 + lane;
   const bool inb = pair < b.npad / 2;
   const bool act0 = inb && proof_active(b, 2 * pair), act1 = inb && proof_active(b, 2 * pair + 1);
   static_assert(ZG_FC_NW == 8, "waves 0..5 carry f, waves 6, 7 load the two lines");
+  const int nlb = (b.npad + 63) / 64, p0 = 2 * blk < nlb ? 2 * blk : nlb - 1, p1 = 2 * blk + 1 < nlb ? 2 * blk + 1 : nlb - 1;
+  // `seen`: steps both producers had published at the last acquire; the f-chain runs ~3x slower
+  // than the R-chain, so after the first steps the wait (and its cache-invalidating acquire)
+  // is skipped
+  int seen = 0;
+  auto wait_lines = [&](int n) {
+    if (!prog || n < seen) return;
+    for (uint32_t it = 0;; it++) {
+      const int d0 = wave_uniform(__hip_atomic_load(&prog[p0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const int d1 = wave_uniform(__hip_atomic_load(&prog[p1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (d0 > n && d1 > n) {
+        seen = d0 < d1 ? d0 : d1;
+        break;
+      }
+      if (wave_uniform(__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+      if (it >= (1u << 19)) {
+        __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  };
   // the pair's two line triples are adjacent in [step][proof][3]
   auto load_lines = [&](int n) {
+    wait_lines(n);
     const Fq2* src = lines + ((size_t)n * b.npad + 2 * (size_t)pair) * 3;
     for (int j = wave - 6; j < 6; j += 2) {
       const bool act = j < 3 ? act0 : act1;
@@ -158,6 +194,31 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, con
     if (wave >= 3) v = f2_neg(v);
     reinterpret_cast<Fq2*>(&b.ftree[b.npad / 2 + pair])[wave] = v;
   }
+}
+// gate (optional): {bfail, fused-wait failure}; the launch is a no-op unless one is set
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines, const int* gate) {
+  if (gate && gate[0] == 0 && gate[1] == 0) return;
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  fchain_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr, nullptr);
+}
+
+// The R-chain and the f-chain as ONE launch for shards whose two grids fit on the device at
+// once (an 8,192-proof rank: 128 lines blocks + 64 f-chain blocks, one block per CU by LDS):
+// blocks [0, P) run the lines of 64 proofs and publish each step (release, agent scope);
+// blocks [P, P + C) run the f-chain of 128 proofs and consume each step as soon as its two
+// lines blocks have published it (acquire). Both kernels alone are latency-bound on a small
+// shard (a block's 68 sequential steps), so overlapping them step by step takes the shorter
+// one off the critical path. Producers never wait; they have the lower block indices and are
+// dispatched first, so the consumers' waits end. proof_active may still see a B that the
+// lines blocks reject (G2 subgroup) as active: bfail then gates the k_batch_fchain re-run.
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_lines_fchain(BatchBufs b, Fq2* lines, int* prog, int* fail) {
+  static_assert(ZG_FCHAIN_SLOTS >= ZG_LINES_SLOTS && ZG_FC_NW >= ZG_LINES_NW, "fused block covers both");
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  const int P = (b.npad + 63) / 64;
+  if ((int)blockIdx.x < P)
+    lines_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, prog);
+  else
+    fchain_body(b, lines, blockIdx.x - P, AtomSpace{lds_atoms}, prog, fail);
 }
 
 // Per-proof Miller leaves ftree[npad + i] for the listed leaf nodes (bisection below a failing
