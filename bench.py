@@ -170,7 +170,7 @@ def main():
     torch.cuda.set_device(local)
 
     from zebra_amd import Context
-    from zebra_amd.dist import combine_partials
+    from zebra_amd.dist import combine_partials, run_pipelined
     src_proofs, src_kinds, idx, kinds, inputs, shard = workload(rank, world, args.n)
     ctx = Context(device=local, max_batch=shard)
     # batches in flight per GPU: each has its own context (buffers + streams); while the host
@@ -200,17 +200,7 @@ def main():
         return ok, c.batch_finish(ok, shard)
 
     def run(k):
-        """k batches, up to len(ctxs) in flight, completed in launch order on every rank"""
-        out, q = [], []
-        for s in range(k):
-            if len(q) == len(ctxs):
-                out.append(complete(q.pop(0)))
-            c = ctxs[s % len(ctxs)]
-            launch(c)
-            q.append(c)
-        while q:
-            out.append(complete(q.pop(0)))
-        return out
+        return run_pipelined(ctxs, k, launch, complete)
 
     def barrier():
         if world > 1:

@@ -95,3 +95,77 @@ def test_two_ranks_one_bad_shard(batch):
     res = _run([_items(good[0:2]), _items([bad[0], good[2]])], False)
     assert [r[1] for r in res] == [False, False]       # verdict broadcast to both ranks
     assert [r[2] for r in res] == [True, False]        # rank 1's own partial localises the failure
+
+
+class _FakeCtx:
+    """stands in for a zg context: batch b's partial is a deterministic 576-byte string"""
+
+    def __init__(self, rank, log):
+        self.rank, self.log, self.batch, self.busy = rank, log, None, False
+
+    def launch(self, b):
+        assert not self.busy, "context relaunched while its batch is in flight"
+        self.busy, self.batch = True, b
+        self.log.append(("launch", b))
+
+    def partial(self):
+        import hashlib
+        return (hashlib.sha256(b"%d/%d" % (self.batch, self.rank)).digest() * 18)[:576]
+
+
+def _pipeline_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from zebra_amd.dist import combine_partials, run_pipelined
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log = []
+        ctxs = [_FakeCtx(rank, log) for _ in range(3)]
+        nxt = [0]
+
+        def launch(c):
+            c.launch(nxt[0])
+            nxt[0] += 1
+
+        def complete(c):
+            # the verdict of batch b: rank 0 sees every rank's partial of that same batch
+            def check(parts):
+                return all(p == _FakeCtx(r, None).__class__.partial(_Probe(c.batch, r)) for r, p in enumerate(parts))
+            ok = combine_partials(c.partial(), check, world, rank, "cpu")
+            c.busy = False
+            log.append(("done", c.batch))
+            return c.batch, ok
+
+        res = run_pipelined(ctxs, 7, launch, complete)
+        q.put((rank, res, log))
+    finally:
+        dist.destroy_process_group()
+
+
+class _Probe:
+    def __init__(self, batch, rank):
+        self.batch, self.rank = batch, rank
+
+
+def test_pipelined_batches_world2():
+    """bench.py's batches in flight: 7 batches, 3 contexts per rank, gloo world 2 -- every batch's
+    gather pairs the two ranks' partials of that same batch, in order, and no context is
+    relaunched while busy"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    got = sorted(q.get(timeout=5) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, res, log in got:
+        assert res == [(b, True) for b in range(7)]
+        assert log[:3] == [("launch", 0), ("launch", 1), ("launch", 2)]
+        assert [e for e in log if e[0] == "done"] == [("done", b) for b in range(7)]

@@ -26,3 +26,20 @@ def combine_partials(partial, check, world, rank, device):
         okt.fill_(1 if check([bytes(p.cpu().numpy().tobytes()) for p in parts]) else 0)
     dist.broadcast(okt, 0)
     return bool(okt.item())
+
+
+def run_pipelined(ctxs, k, launch, complete):
+    """k batches with up to len(ctxs) in flight (one context each, round-robin): a context is
+    relaunched only after its previous batch completed, and batches complete in launch order
+    on every rank, so the per-batch collectives of `complete` (combine_partials) line up across
+    ranks. Returns the k results of complete(ctx) in batch order."""
+    out, q = [], []
+    for s in range(k):
+        if len(q) == len(ctxs):
+            out.append(complete(q.pop(0)))
+        c = ctxs[s % len(ctxs)]
+        launch(c)
+        q.append(c)
+    while q:
+        out.append(complete(q.pop(0)))
+    return out
