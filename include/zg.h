@@ -20,7 +20,10 @@
  *        rank produces one 576-byte Miller partial, gathered over RCCL, one final exp.
  *
  * Threading: calls on different contexts are independent; one call at a time per
- * context (internal mutex). Every context owns its HIP stream and device buffers.
+ * context (internal mutex). Every context owns its HIP streams and device buffers, so
+ * several contexts on one GPU keep several batches in flight (zg_batch_begin returns once
+ * the batch is queued). ZG_LINES_FCHAIN (environment, read by zg_create): unset = pick the
+ * R-chain/f-chain launch shape by size, 0 = two launches, 1 = one fused launch.
  */
 #ifndef ZG_H
 #define ZG_H
