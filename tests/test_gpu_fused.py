@@ -72,3 +72,36 @@ def test_partials_equal(ctxs, n):
         assert c.gt_check([parts[-1]])
         assert c.batch_finish(True, n) == [0] * n
     assert parts[0] == parts[1]
+
+
+def test_batches_in_flight_match_sequential():
+    """three contexts with batches queued together on one GPU (bench.py's batches in flight)
+    give the same Miller partials and statuses as one batch at a time"""
+    from zebra_amd import Context, pack_inputs
+    real = load_golden("real_proofs.json")["proofs"]
+    src_proofs = b"".join(bytes.fromhex(e["proof"]) for e in real)
+    src_kinds = bytes(e["kind"] for e in real)
+    n = 2048
+    cs = [Context(device=0, max_batch=n, seed=11) for _ in range(3)]
+    try:
+        batches = []
+        for b in range(3):
+            idx = [(i + b) % len(real) for i in range(n)]
+            proofs = cs[0].synth_rerandomize(src_proofs, src_kinds, idx, 20 + b)
+            kinds = bytes(src_kinds[j] for j in idx)
+            inputs = pack_inputs([[bytes.fromhex(x) for x in real[j]["inputs"]] for j in idx])
+            batches.append((proofs, kinds, inputs))
+        seq = []
+        for b in range(3):
+            cs[0].batch_begin(*batches[b])
+            seq.append(cs[0].batch_partial())
+            assert cs[0].batch_finish(True, n) == [0] * n
+        for b in range(3):
+            cs[b].batch_begin(*batches[b])
+        for b in range(3):
+            assert cs[b].batch_partial() == seq[b]
+            assert cs[b].gt_check([seq[b]])
+            assert cs[b].batch_finish(True, n) == [0] * n
+    finally:
+        for c in cs:
+            c.close()
