@@ -145,9 +145,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=65536, help="total proofs per step (all ranks)")
+    ap.add_argument("--proofs", "--n", dest="n", type=int, default=65536, help="total proofs per step (all ranks)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU, one context each (0: 3 for shards > 16k proofs, else 6)")
+    ap.add_argument("--dist", action="store_true", help="use torch.distributed (RCCL) even at world size 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 side measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -157,6 +158,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --dist: the RCCL path even at world size 1 (a 1-GPU rehearsal of the multi-GPU protocol)
+    use_dist = world > 1 or args.dist
     if args.inflight <= 0:
         args.inflight = 3 if args.n // world > 16384 else 6
     # two streams per context (main + side): give each its own hardware queue (set before the
@@ -165,8 +168,19 @@ def main():
     os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch
     import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if use_dist:
+        # RCCL prints its version banner on stdout while it initialises: keep stdout for the one
+        # JSON line (fd-level, the banner comes from C)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     torch.cuda.set_device(local)
 
     from zebra_amd import Context
@@ -193,7 +207,7 @@ def main():
     def complete(c):
         part = c.batch_partial()
         timings.append(c.last_timings())
-        if world > 1:   # RCCL over xGMI: 576 B per GPU, ONE final exponentiation on rank 0
+        if use_dist:   # RCCL over xGMI: 576 B per GPU, ONE final exponentiation on rank 0
             ok = combine_partials(part, c.gt_check, world, rank, dev)
         else:
             ok = c.gt_check([part])
@@ -203,7 +217,7 @@ def main():
         return run_pipelined(ctxs, k, launch, complete)
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -215,7 +229,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -281,7 +295,7 @@ def main():
         print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

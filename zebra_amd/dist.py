@@ -1,6 +1,7 @@
 """Multi-GPU protocol (one process per GPU, torch.distributed; backend "nccl" is RCCL on
-ROCm): contiguous shards, one 576-byte Miller partial per rank, all-gather, ONE final
-exponentiation on rank 0, verdict broadcast. SURVEY.md 8(e); DESIGN.md section 6."""
+ROCm): contiguous shards, one 576-byte Miller partial per rank, all-gather, the final
+exponentiation of their product on every rank (same inputs, same verdict). SURVEY.md 8(e);
+DESIGN.md section 6."""
 
 GT_BYTES = 576
 
@@ -13,19 +14,20 @@ def shard_range(n, world, rank):
 
 
 def combine_partials(partial, check, world, rank, device):
-    """All-gather every rank's 576-byte partial; rank 0 runs `check(list_of_partials) -> bool`
-    (one final exponentiation of their product); the verdict is broadcast to every rank."""
+    """All-gather every rank's 576-byte partial (one RCCL all-gather into one tensor, one copy
+    back) and run `check(list_of_partials) -> bool` -- ONE final exponentiation of their
+    product -- on every rank: all ranks hold the same partials, so they reach the same verdict
+    without a second collective (ncclAllGather when every rank needs the result).
+    Keeping the exchange to one collective matters with batches in flight: every extra device
+    op queues behind the other batches' kernels."""
     import torch
     import torch.distributed as dist
     assert len(partial) == GT_BYTES
     mine = torch.frombuffer(bytearray(partial), dtype=torch.uint8).to(device)
-    parts = [torch.empty(GT_BYTES, dtype=torch.uint8, device=device) for _ in range(world)]
-    dist.all_gather(parts, mine)
-    okt = torch.zeros(1, dtype=torch.int32, device=device)
-    if rank == 0:
-        okt.fill_(1 if check([bytes(p.cpu().numpy().tobytes()) for p in parts]) else 0)
-    dist.broadcast(okt, 0)
-    return bool(okt.item())
+    flat = torch.empty(world * GT_BYTES, dtype=torch.uint8, device=device)
+    dist.all_gather_into_tensor(flat, mine)
+    allb = flat.cpu().numpy().tobytes()
+    return check([allb[GT_BYTES * r:GT_BYTES * (r + 1)] for r in range(world)])
 
 
 def run_pipelined(ctxs, k, launch, complete):
