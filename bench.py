@@ -204,14 +204,21 @@ def main():
     def launch(c):
         c.batch_begin_device(shard, d_proofs.data_ptr(), d_kinds.data_ptr(), d_inputs.data_ptr())
 
+    host = []   # per batch: host seconds waiting for the partial, in the exchange + check, in finish
+
     def complete(c):
+        t0 = time.perf_counter()
         part = c.batch_partial()
         timings.append(c.last_timings())
-        if use_dist:   # RCCL over xGMI: 576 B per GPU, ONE final exponentiation on rank 0
+        t1 = time.perf_counter()
+        if use_dist:   # RCCL over xGMI: 576 B per GPU, the final exponentiation of their product
             ok = combine_partials(part, c.gt_check, world, rank, dev)
         else:
             ok = c.gt_check([part])
-        return ok, c.batch_finish(ok, shard)
+        t2 = time.perf_counter()
+        sts = c.batch_finish(ok, shard)
+        host.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
+        return ok, sts
 
     def run(k):
         return run_pipelined(ctxs, k, launch, complete)
@@ -223,6 +230,7 @@ def main():
 
     run(args.warmup)
     timings.clear()
+    host.clear()
     barrier()
     t0 = time.perf_counter()
     results = run(args.steps)
@@ -236,6 +244,7 @@ def main():
     for ok, sts in results:
         assert ok and all(s == 0 for s in sts), "valid synthetic batch rejected"
 
+    host_ms = [1e3 * sum(h[i] for h in host) / len(host) for i in range(3)]
     # isolated launches (one batch in flight, after the timed region): the kernels' own roofline
     iso = []
     for _ in range(3):
@@ -284,6 +293,8 @@ def main():
                               "note": "3 batches with one in flight after the timed region: a launch alone on the GPU"},
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
+        "host_ms_per_batch": {"wait_partial": host_ms[0], "exchange_and_final_exp": host_ms[1],
+                              "statuses": host_ms[2]},
     }
     if rank == 0 and world == 1 and not args.no_configs:
         out["other_configs"] = other_configs(ctx, src_proofs, src_kinds)
