@@ -149,6 +149,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU, one context each (0: 3 for shards > 16k proofs, else 6)")
     ap.add_argument("--dist", action="store_true", help="use torch.distributed (RCCL) even at world size 1")
+    ap.add_argument("--no-iso", action="store_true", help="skip the isolated-launch pass (profiling the timed launches)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 side measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -247,7 +248,7 @@ def main():
     host_ms = [1e3 * sum(h[i] for h in host) / len(host) for i in range(3)]
     # isolated launches (one batch in flight, after the timed region): the kernels' own roofline
     iso = []
-    for _ in range(3):
+    for _ in range(0 if args.no_iso else 3):
         launch(ctx)
         ok_, sts_ = complete(ctx)
         iso.append(timings.pop())
@@ -263,6 +264,8 @@ def main():
     # shard runs them fused -- its lines phase is then empty), algorithmic MACs per launch over
     # its mean launch duration (HIP events, timed region; with batches in flight a launch shares
     # the device with the other batch's kernels)
+    if not iso:
+        iso = timings
     fused = iso[0][1] < 0.05   # the fused launch leaves the lines phase empty (isolated pass)
     rk, wk = ("k_lines_fchain", W_LINES + W_FCHAIN) if fused else ("k_batch_fchain", W_FCHAIN)
     achieved = wk * MACS_PER_FQMUL * shard / (avg[2] * 1e-3)
