@@ -293,7 +293,8 @@ def main():
         "roofline_isolated": {"kernel": rk, "achieved": iso_achieved / 1e12, "frac": iso_achieved / peak,
                               "kernel_ms": iso_avg[2], "phase_ms": dict(zip(names, iso_avg)),
                               "phase_frac": phase_frac,
-                              "note": "3 batches with one in flight after the timed region: a launch alone on the GPU"},
+                              "note": "no isolated pass (--no-iso): same launches as roofline" if args.no_iso else
+                                      "3 batches with one in flight after the timed region: a launch alone on the GPU"},
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
         "host_ms_per_batch": {"wait_partial": host_ms[0], "exchange_and_final_exp": host_ms[1],
