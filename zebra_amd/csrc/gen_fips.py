@@ -210,6 +210,48 @@ def main():
     out.append("  mp_reduce_once<12>(r, t, pm);")
     out.append("}")
     out.append("")
+    # ---- lazy-reduction building blocks: the 24-limb product and the Montgomery reduction of a
+    # 24-limb value, the same column statements split in two (an Fq2 Karatsuba product reduces
+    # twice instead of three times: zg_prog.h f2_mul_kind)
+    out += ["// t = a * b (24 limbs, no reduction)",
+            "__device__ __forceinline__ void fq_mul_wide(uint32_t* t, const uint32_t* a, const uint32_t* b) {",
+            "  uint64_t lm = 0, c0, c1;", "  uint32_t h = 0;"]
+    for i in range(2 * N - 1):
+        prods = [("a[%d]" % j, "b[%d]" % (i - j)) for j in range(max(0, i - N + 1), min(i, N - 1) + 1)]
+        out.append(column(prods, "column %d" % i))
+        out.append("  t[%d] = (uint32_t)lm;" % i)
+        out.append("  lm = (lm >> 32) | ((uint64_t)h << 32);")
+        out.append("  h = 0;")
+    out.append("  t[%d] = (uint32_t)lm;" % (2 * N - 1))
+    out.append("}")
+    out.append("")
+    out += ["// r = t * 2^-384 mod p for t < 2^384 p (24 limbs)  ->  r < p",
+            "__device__ __forceinline__ void fq_redc_wide(uint32_t* r, const uint32_t* t) {",
+            "  uint32_t m[12], u[12];", "  uint64_t lm = 0, c0, c1;", "  uint32_t h = 0;"]
+    for i in range(N):
+        out.append("  lm += t[%d];  // lm < 2^38 here: no overflow" % i)
+        prods = [("m[%d]" % j, "FQ_P[%d]" % (i - j)) for j in range(i)]
+        if prods:
+            out.append(column(prods, "column %d: m p products" % i))
+        out.append("  m[%d] = (uint32_t)lm * FQ_INV;" % i)
+        out.append(column([("m[%d]" % i, "FQ_P[0]")], "column %d: m_%d p_0" % (i, i)))
+        out.append("  lm = (lm >> 32) | ((uint64_t)h << 32);")
+        out.append("  h = 0;")
+    for i in range(N, 2 * N - 1):
+        out.append("  lm += t[%d];" % i)
+        prods = [("m[%d]" % j, "FQ_P[%d]" % (i - j)) for j in range(i - N + 1, N)]
+        out.append(column(prods, "column %d" % i))
+        out.append("  u[%d] = (uint32_t)lm;" % (i - N))
+        out.append("  lm = (lm >> 32) | ((uint64_t)h << 32);")
+        out.append("  h = 0;")
+    out.append("  lm += t[%d];" % (2 * N - 1))
+    out.append("  u[11] = (uint32_t)lm;  // < 2p < 2^382: no further carry")
+    out.append("  uint32_t pm[12];")
+    out.append("#pragma unroll")
+    out.append("  for (int i = 0; i < 12; i++) pm[i] = FQ_P[i];")
+    out.append("  mp_reduce_once<12>(r, u, pm);")
+    out.append("}")
+    out.append("")
     out.append("// ---- Fq add / sub carry chains, one asm statement each (interleaved chains, see above)")
     for name, kinds in FQ_FNS:
         out += fq_ops_fn(name, kinds)
