@@ -7,15 +7,17 @@ config 3: 65,536 mixed spend/output proofs), on N MI355X, one process per GPU.
 A step = one batch verification of the whole 65,536-proof workload: every rank verifies its
 contiguous shard (decode + subgroup checks + batch algebra + per-proof Miller loops + product
 tree) from HBM-resident inputs, emits one 576-byte Miller partial, the partials are gathered
-over RCCL, rank 0 runs ONE final exponentiation, the verdict is broadcast and every rank
-finalises its per-proof statuses. Inputs: real mainnet proofs from the reference's fixtures,
+over RCCL (one all-gather), every rank runs the ONE final exponentiation of their product on the
+same gathered bytes (same verdict, no second collective) and finalises its per-proof statuses. Inputs: real mainnet proofs from the reference's fixtures,
 re-randomized on the GPU (synthetic, all valid; verified OK after the timed region).
 Batch scalars r_i come from the OS RNG inside the timed region (production mode).
-Batches in flight (--inflight, default 2): each GPU keeps that many consecutive batches on the
-device, one context (buffers + streams) each, so the next batch's kernels run while the host
-waits on the oldest one's partial, gather, verdict and statuses. Every batch is fully verified
-and completed in order inside the timed region (pipeline fill and drain included); a batch's
-own latency is phase_ms.device_pipeline plus the final exponentiation.
+Batches in flight (--inflight; default 3, or 6 on shards <= 16k proofs): each GPU keeps that many
+consecutive batches on the device, one context (buffers + streams) each. The host reads the
+oldest batch's partial and statuses and relaunches its context at once; the batch's verdict
+(gather + final exponentiation, on a checker context) runs on a worker thread in batch order
+(--sync-verdict: before the relaunch). Every batch is fully verified and its verdict is in
+inside the timed region (pipeline fill and drain included); a false verdict re-runs the batch
+with bisection. A batch's own latency is phase_ms.device_pipeline plus the final exponentiation.
 """
 import argparse
 import json
@@ -148,6 +150,10 @@ def main():
     ap.add_argument("--proofs", "--n", dest="n", type=int, default=65536, help="total proofs per step (all ranks)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU, one context each (0: 3 for shards > 16k proofs, else 6)")
+    ap.add_argument("--sync-verdict", action="store_true",
+                    help="take each batch's verdict (gather + final exponentiation) before relaunching its context")
+    ap.add_argument("--no-priority", action="store_true",
+                    help="default-priority streams for the checker context and RCCL")
     ap.add_argument("--dist", action="store_true", help="use torch.distributed (RCCL) even at world size 1")
     ap.add_argument("--no-iso", action="store_true", help="skip the isolated-launch pass (profiling the timed launches)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -162,7 +168,9 @@ def main():
     # --dist: the RCCL path even at world size 1 (a 1-GPU rehearsal of the multi-GPU protocol)
     use_dist = world > 1 or args.dist
     if args.inflight <= 0:
-        args.inflight = 3 if args.n // world > 16384 else 6
+        # at most 6 contexts per process (7 fail with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box,
+        # whatever the queue count): deferred verdicts spend one on the checker
+        args.inflight = (3 if args.n // world > 16384 else 6) - (0 if args.sync_verdict else 1)
     # two streams per context (main + side): give each its own hardware queue (set before the
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     hwq = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 12))
@@ -176,7 +184,11 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            opts = None
+            if not args.no_priority:   # the 576-B gathers jump the queue of in-flight batches' blocks
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
             dist.barrier()
         finally:
             sys.stdout.flush()
@@ -185,12 +197,18 @@ def main():
     torch.cuda.set_device(local)
 
     from zebra_amd import Context
-    from zebra_amd.dist import combine_partials, run_pipelined
+    from zebra_amd.dist import combine_partials, run_pipelined, run_pipelined_deferred
     src_proofs, src_kinds, idx, kinds, inputs, shard = workload(rank, world, args.n)
     ctx = Context(device=local, max_batch=shard)
     # batches in flight per GPU: each has its own context (buffers + streams); while the host
     # waits on the oldest batch's partial / verdict, the next one is already on the device
     ctxs = [ctx] + [Context(device=local, max_batch=shard) for _ in range(args.inflight - 1)]
+    # the verdicts (gather + final exponentiation) run on a checker context of their own, on a
+    # worker thread in batch order, so a batch context is relaunched as soon as its partial and
+    # statuses are read (zebra_amd.dist.run_pipelined_deferred)
+    checker = None if args.sync_verdict else Context(device=local, max_batch=64)
+    if checker and not args.no_priority:
+        checker.set_priority(True)
     t0 = time.perf_counter()
     proofs = ctx.synth_rerandomize(src_proofs, src_kinds, idx, 2 + 1000003 * rank)
     log("rank %d: generated %d re-randomized proofs in %.1f s" % (rank, shard, time.perf_counter() - t0))
@@ -207,22 +225,47 @@ def main():
 
     host = []   # per batch: host seconds waiting for the partial, in the exchange + check, in finish
 
+    def check(part, on):
+        if use_dist:   # RCCL over xGMI: 576 B per GPU, the final exponentiation of their product
+            return combine_partials(part, on.gt_check, world, rank, dev)
+        return on.gt_check([part])
+
     def complete(c):
         t0 = time.perf_counter()
         part = c.batch_partial()
         timings.append(c.last_timings())
         t1 = time.perf_counter()
-        if use_dist:   # RCCL over xGMI: 576 B per GPU, the final exponentiation of their product
-            ok = combine_partials(part, c.gt_check, world, rank, dev)
-        else:
-            ok = c.gt_check([part])
+        ok = check(part, c)
         t2 = time.perf_counter()
         sts = c.batch_finish(ok, shard)
         host.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
         return ok, sts
 
+    def harvest(c):
+        t0 = time.perf_counter()
+        part = c.batch_partial()
+        timings.append(c.last_timings())
+        t1 = time.perf_counter()
+        sts = c.batch_finish(True, shard)   # provisional: a false verdict re-runs the batch (redo)
+        host.append((t1 - t0, 0.0, time.perf_counter() - t1))
+        return part, sts
+
+    def verdict(part):
+        t0 = time.perf_counter()
+        ok = check(part, checker)
+        vtime.append(time.perf_counter() - t0)
+        return ok
+
+    def redo(_s):
+        launch(ctx)
+        return complete(ctx)[1]
+
+    vtime = []
+
     def run(k):
-        return run_pipelined(ctxs, k, launch, complete)
+        if args.sync_verdict:
+            return run_pipelined(ctxs, k, launch, complete)
+        return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo)
 
     def barrier():
         if use_dist:
@@ -232,6 +275,7 @@ def main():
     run(args.warmup)
     timings.clear()
     host.clear()
+    vtime.clear()
     barrier()
     t0 = time.perf_counter()
     results = run(args.steps)
@@ -246,6 +290,8 @@ def main():
         assert ok and all(s == 0 for s in sts), "valid synthetic batch rejected"
 
     host_ms = [1e3 * sum(h[i] for h in host) / len(host) for i in range(3)]
+    if vtime:   # deferred verdicts: the worker thread's time per batch (overlaps the next batches)
+        host_ms[1] = 1e3 * sum(vtime) / len(vtime)
     # isolated launches (one batch in flight, after the timed region): the kernels' own roofline
     iso = []
     for _ in range(0 if args.no_iso else 3):
@@ -298,7 +344,8 @@ def main():
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
         "host_ms_per_batch": {"wait_partial": host_ms[0], "exchange_and_final_exp": host_ms[1],
-                              "statuses": host_ms[2]},
+                              "statuses": host_ms[2],
+                              "verdict": "sync" if args.sync_verdict else "deferred (worker thread, checker context)"},
     }
     if rank == 0 and world == 1 and not args.no_configs:
         out["other_configs"] = other_configs(ctx, src_proofs, src_kinds)
@@ -308,7 +355,7 @@ def main():
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for c in ctxs:
+    for c in ctxs + ([checker] if checker else []):
         c.close()
     if use_dist:
         dist.destroy_process_group()

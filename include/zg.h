@@ -130,6 +130,11 @@ int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const voi
 int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
 int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
 int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);
+/* zg_set_priority: recreate the context's two streams at the device's highest (high != 0) or
+ * default priority; only between batches. A context that only runs zg_gt_check (the verdict of
+ * batches kept in flight on other contexts) gets its final exponentiation dispatched ahead of
+ * their waiting workgroups. */
+int zg_set_priority(zg_ctx* ctx, int high);
 
 /* ---- host-side public-input preparation (CPU; no context, no GPU). The reference does this
  * in Rust before calling bellman; these restate it so a caller can go from description bytes

@@ -169,3 +169,72 @@ def test_pipelined_batches_world2():
         assert res == [(b, True) for b in range(7)]
         assert log[:3] == [("launch", 0), ("launch", 1), ("launch", 2)]
         assert [e for e in log if e[0] == "done"] == [("done", b) for b in range(7)]
+
+
+def _deferred_worker(rank, world, port, q):
+    import sys
+    import threading
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from zebra_amd.dist import combine_partials, run_pipelined_deferred
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log, bad = [], 4   # batch 4's partial on rank 1 is corrupted: that batch's verdict is false
+        ctxs = [_FakeCtx(rank, log) for _ in range(3)]
+        nxt = [0]
+
+        def launch(c):
+            c.launch(nxt[0])
+            nxt[0] += 1
+
+        def harvest(c):
+            part = c.partial() if not (c.batch == bad and rank == 1) else bytes(576)
+            c.busy = False
+            log.append(("harvest", c.batch))
+            return (c.batch, part), ["provisional", c.batch]
+
+        def verdict(item):
+            b, part = item
+            assert threading.current_thread() is not threading.main_thread()
+            log.append(("verdict", b))
+
+            def check(parts):
+                return all(p == _FakeCtx.partial(_Probe(b, r)) for r, p in enumerate(parts))
+            return combine_partials(part, check, world, rank, "cpu")
+
+        def redo(s):
+            log.append(("redo", s))
+            return ["bisected", s]
+
+        res = run_pipelined_deferred(ctxs, 7, launch, harvest, verdict, redo)
+        q.put((rank, res, log))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_deferred_verdicts_world2():
+    """bench.py's default schedule: a context is relaunched right after its partial and statuses
+    are read, the verdicts (the all-gather + check) run on one worker thread in batch order on
+    both ranks, and a batch with a false verdict gets redo()'s statuses on every rank"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_deferred_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    got = sorted(q.get(timeout=5) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for rank, res, log in got:
+        assert res == [(b != 4, ["provisional" if b != 4 else "bisected", b]) for b in range(7)]
+        assert [e for e in log if e[0] == "verdict"] == [("verdict", b) for b in range(7)]
+        assert [e for e in log if e[0] == "harvest"] == [("harvest", b) for b in range(7)]
+        assert [e for e in log if e[0] == "redo"] == [("redo", 4)]
+        # the 4th launch (batch 3) reuses the first context right after batch 0's harvest,
+        # without waiting for batch 0's verdict (the worker thread logs verdicts concurrently)
+        main = [e for e in log if e[0] != "verdict"]
+        assert main.index(("launch", 3)) == main.index(("harvest", 0)) + 1

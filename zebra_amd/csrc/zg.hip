@@ -630,6 +630,24 @@ extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, i
   return ZG_OK;
 }
 
+extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
+  if (!ctx) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->state != 0) return fail(ctx, ZG_E_STATE, "zg_set_priority with a batch in flight");
+  HIPCHK(hipSetDevice(ctx->device));
+  int lo = 0, hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->side));
+  HIPCHK(hipStreamDestroy(ctx->stream));
+  HIPCHK(hipStreamDestroy(ctx->side));
+  ctx->stream = ctx->side = nullptr;
+  const int prio = high ? hi : lo;  // numerically lower = higher priority (hi <= lo)
+  HIPCHK(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio));
+  HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio));
+  return ZG_OK;
+}
+
 // Bisection over the product trees: a failing node's children are re-checked exactly;
 // a failing leaf is a proof whose own check fails (r_i != 0 makes it bellman's check).
 static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {

@@ -45,3 +45,34 @@ def run_pipelined(ctxs, k, launch, complete):
     while q:
         out.append(complete(q.pop(0)))
     return out
+
+
+def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo):
+    """run_pipelined with the verdict taken off the context's critical path.
+
+    harvest(ctx) -> (partial, statuses) waits for a batch's Miller partial and reads its
+    per-proof statuses as if the batch verdict were true (decode rejects and input-count
+    errors are final either way); the context is then free and is relaunched at once.
+    verdict(partial) -> bool (the all-gather + ONE final exponentiation, on a checker context
+    of its own) runs on a single worker thread in batch order, so the per-batch collectives
+    line up across ranks exactly as in run_pipelined. A batch whose verdict is false is
+    re-verified by redo(batch_index) -> statuses (bisection on a fresh pass: per-proof
+    results do not depend on the batch scalars) after the pipeline has drained. Returns the k
+    (verdict, statuses) pairs in batch order; all verdicts are in before it returns."""
+    from concurrent.futures import ThreadPoolExecutor
+    pend, q = [], []
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        def take():
+            s, c = q.pop(0)
+            part, sts = harvest(c)
+            pend.append((s, sts, ex.submit(verdict, part)))
+        for s in range(k):
+            if len(q) == len(ctxs):
+                take()
+            c = ctxs[s % len(ctxs)]
+            launch(c)
+            q.append((s, c))
+        while q:
+            take()
+        oks = [f.result() for _, _, f in pend]
+    return [(ok, sts if ok else redo(s)) for ok, (s, sts, _) in zip(oks, pend)]

@@ -38,6 +38,7 @@ def lib():
         vp, u8p, sz, i = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int
         L.zg_create.restype = vp
         L.zg_create.argtypes = [ctypes.POINTER(_Config)]
+        L.zg_set_priority.argtypes = [vp, i]
         L.zg_destroy.argtypes = [vp]
         L.zg_last_error.restype = ctypes.c_char_p
         L.zg_last_error.argtypes = [vp]
@@ -220,6 +221,10 @@ class Context:
         ok = ctypes.c_int(0)
         self._chk(lib().zg_gt_check(self._p, len(partials), b"".join(partials), ctypes.byref(ok)))
         return bool(ok.value)
+
+    def set_priority(self, high):
+        """recreate this context's streams at the highest (True) or default priority"""
+        self._chk(lib().zg_set_priority(self._p, 1 if high else 0))
 
     def batch_finish(self, batch_ok, n):
         st = ctypes.create_string_buffer(max(n, 1))
