@@ -13,20 +13,45 @@ def shard_range(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+_xbufs = {}
+
+
+def _exchange_buffers(world, device):
+    """per (device, world): the staging buffers of combine_partials, allocated once (pinned host
+    memory and a high-priority stream on a GPU, so the 576-B copies are DMA enqueues that do not
+    wait behind in-flight batches)"""
+    import torch
+    key = (str(device), world)
+    if key not in _xbufs:
+        gpu = torch.device(device).type == "cuda"
+        stream = torch.cuda.Stream(device=device, priority=-1) if gpu else None
+        _xbufs[key] = (torch.empty(GT_BYTES, dtype=torch.uint8, pin_memory=gpu),
+                       torch.empty(GT_BYTES, dtype=torch.uint8, device=device),
+                       torch.empty(world * GT_BYTES, dtype=torch.uint8, device=device),
+                       torch.empty(world * GT_BYTES, dtype=torch.uint8, pin_memory=gpu), stream)
+    return _xbufs[key]
+
+
 def combine_partials(partial, check, world, rank, device):
     """All-gather every rank's 576-byte partial (one RCCL all-gather into one tensor, one copy
     back) and run `check(list_of_partials) -> bool` -- ONE final exponentiation of their
     product -- on every rank: all ranks hold the same partials, so they reach the same verdict
     without a second collective (ncclAllGather when every rank needs the result).
     Keeping the exchange to one collective matters with batches in flight: every extra device
-    op queues behind the other batches' kernels."""
+    op queues behind the other batches' kernels. Calls must not overlap (the staging buffers are
+    reused; run_pipelined* issue them from one thread, in batch order)."""
+    import contextlib
+    import numpy as np
     import torch
     import torch.distributed as dist
     assert len(partial) == GT_BYTES
-    mine = torch.frombuffer(bytearray(partial), dtype=torch.uint8).to(device)
-    flat = torch.empty(world * GT_BYTES, dtype=torch.uint8, device=device)
-    dist.all_gather_into_tensor(flat, mine)
-    allb = flat.cpu().numpy().tobytes()
+    host, mine, flat, back, stream = _exchange_buffers(world, device)
+    with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+        host.numpy()[:] = np.frombuffer(partial, dtype=np.uint8)
+        mine.copy_(host, non_blocking=True)
+        dist.all_gather_into_tensor(flat, mine)
+        back.copy_(flat)
+    allb = back.numpy().tobytes()
     return check([allb[GT_BYTES * r:GT_BYTES * (r + 1)] for r in range(world)])
 
 
