@@ -11,9 +11,9 @@ for n in 8192 65536; do
     flag=""; [ $mode = sync ] && flag="--sync-verdict"
     [ $mode = deferred4 ] && flag="--inflight 4"
     [ $mode = deferred4 ] && [ $n = 8192 ] && continue
-    timeout -k 10 150 python -u bench.py --no-cpu --no-configs --no-iso --n $n $flag > $O/b_${n}_$mode.json 2> $O/b_${n}_$mode.err || { echo "bench $n $mode failed"; tail -20 $O/b_${n}_$mode.err; exit 1; }
+    timeout -k 10 150 python -u bench.py --no-cpu --no-configs --no-iso --proofs $n $flag > $O/b_${n}_$mode.json 2> $O/b_${n}_$mode.err || { echo "bench $n $mode failed"; tail -20 $O/b_${n}_$mode.err; exit 1; }
     show $O/b_${n}_$mode.json "$n $mode"
   done
 done
-timeout -k 10 150 python -u bench.py --no-cpu --no-configs --no-iso --dist --n 8192 > $O/b_8192_dist.json 2> $O/b_8192_dist.err || { echo "bench dist failed"; tail -20 $O/b_8192_dist.err; exit 1; }
+timeout -k 10 180 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --no-cpu --no-configs --no-iso --dist --proofs 8192 > $O/b_8192_dist.json 2> $O/b_8192_dist.err || { echo "bench dist failed"; tail -20 $O/b_8192_dist.err; exit 1; }
 show $O/b_8192_dist.json "8192 dist-deferred"
