@@ -20,10 +20,17 @@
  *        rank produces one 576-byte Miller partial, gathered over RCCL, one final exp.
  *
  * Threading: calls on different contexts are independent; one call at a time per
- * context (internal mutex). Every context owns its HIP streams and device buffers, so
- * several contexts on one GPU keep several batches in flight (zg_batch_begin returns once
- * the batch is queued). ZG_LINES_FCHAIN (environment, read by zg_create): unset = pick the
- * R-chain/f-chain launch shape by size, 0 = two launches, 1 = one fused launch.
+ * context (internal mutex; zg_verify_batch holds it from begin to finish). A context is a
+ * BATCH SLOT: it owns device buffers only. The HIP streams (a fixed pool of stream pairs per
+ * device, ZG_STREAM_PAIRS, default 8) and the prepared verifying keys (prepare_verifying_key
+ * once per distinct key per device) belong to a per-device state shared by all contexts of the
+ * process, so any number of slots can be created without new hardware queues. Slots keep
+ * several batches in flight on one GPU (zg_batch_begin returns once the batch is queued);
+ * slot i uses pair i mod ZG_STREAM_PAIRS. HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+ * queues (HIP default 4): the library is correct at any value; for batches in flight to
+ * overlap, set GPU_MAX_HW_QUEUES >= 2 x (pairs in use) + 2 before the HIP runtime starts.
+ * ZG_LINES_FCHAIN (environment, read by zg_create): unset = pick the R-chain/f-chain launch
+ * shape by size, 0 = two launches, 1 = one fused launch.
  */
 #ifndef ZG_H
 #define ZG_H
@@ -78,6 +85,8 @@ typedef struct zg_config {
 
 typedef struct zg_ctx zg_ctx;
 
+/* NULL on failure (no device, out of device memory, HIP error); zg_last_error(NULL) then
+ * describes it (per calling thread). */
 zg_ctx* zg_create(const zg_config* cfg);
 void zg_destroy(zg_ctx* ctx);
 const char* zg_last_error(zg_ctx* ctx);
@@ -177,6 +186,12 @@ int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, c
  * [5] side stream (C/Fr trees + VK-side MSM + VK Miller loops, overlapping [2]-[3]),
  * [6] whole device pipeline */
 int zg_last_timings(zg_ctx* ctx, float* ms7);
+/* cumulative counters of this context: [0] batches, [1] fused R-chain + f-chain launches,
+ * [2] fused launches whose consumers timed out waiting (the f-chain was recomputed by the
+ * split kernel; the context uses split launches from then on), [3] batches with a B that
+ * failed its G2 subgroup check (gated recompute of the VK-side root work), [4] bisections,
+ * [5] tree nodes checked by bisection. Writes min(n, 6) values, zero beyond. */
+int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.
  * This entry runs the same device block function for known-answer tests: out = nblocks x 64 B
@@ -185,6 +200,9 @@ int zg_chacha20_blocks(zg_ctx* ctx, const uint8_t key[32], const uint8_t nonce[1
                        size_t nblocks, uint8_t* out);
 /* microbenchmark: v_mad_u64_u32 chains; returns achieved 32x32->64 MACs per second */
 int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s);
+/* the same probe, plus the shader clock it ran at (median over workgroups of s_memtime ticks
+ * per 100 MHz s_memrealtime tick, stamped around the loop); clock_hz may be NULL */
+int zg_bench_mad_rate_clock(zg_ctx* ctx, double* macs_per_s, double* clock_hz);
 
 #ifdef __cplusplus
 }

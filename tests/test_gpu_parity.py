@@ -185,3 +185,49 @@ def test_partial_bitexact_vs_oracle(ctx):
                                    [int.from_bytes(bytes.fromhex(x), "little") for x in e["inputs"]],
                                    G.batch_r(bytes.fromhex(e["r"]))) for e in items])
     assert part == B.f12_to_bytes(want)
+
+
+def test_batch_state_errors(ctx):
+    """a second zg_batch_begin while a batch is in flight is ZG_E_STATE (the first
+    batch is not silently discarded); finishing it then works; finish without begin is
+    ZG_E_STATE too"""
+    from zebra_amd.zg import ZgError
+    items = load_golden("real_proofs.json")["proofs"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    ctx.batch_begin(proofs, kinds, inputs, nin)
+    with pytest.raises(ZgError) as e:
+        ctx.batch_begin(proofs, kinds, inputs, nin)
+    assert e.value.code == -6
+    part = ctx.batch_partial()
+    assert ctx.gt_check([part])
+    assert ctx.batch_finish(True, len(items)) == [0] * len(items)
+    with pytest.raises(ZgError) as e:
+        ctx.batch_finish(True, len(items))
+    assert e.value.code == -6
+
+
+def test_many_slots_in_flight():
+    """20 contexts (batch slots) on one GPU, all with a batch in flight at once: the slots share
+    the device's fixed stream pool and its prepared VKs (no stream or queue per slot), and
+    every batch verifies"""
+    from zebra_amd import Context, pack_inputs
+    real = load_golden("real_proofs.json")["proofs"]
+    src_proofs = b"".join(bytes.fromhex(e["proof"]) for e in real)
+    src_kinds = bytes(e["kind"] for e in real)
+    n = 256
+    cs = [Context(device=0, max_batch=n) for _ in range(20)]
+    try:
+        idx = [i % len(real) for i in range(n)]
+        proofs = cs[0].synth_rerandomize(src_proofs, src_kinds, idx, 31)
+        kinds = bytes(src_kinds[j] for j in idx)
+        inputs = pack_inputs([[bytes.fromhex(x) for x in real[j]["inputs"]] for j in idx])
+        for c in cs:
+            c.batch_begin(proofs, kinds, inputs)
+        parts = [c.batch_partial() for c in cs]
+        for c, p in zip(cs, parts):
+            assert c.gt_check([p])
+            assert c.batch_finish(True, n) == [0] * n
+        assert len(set(parts)) == 20   # independent OS-random batch scalars per batch
+    finally:
+        for c in cs:
+            c.close()

@@ -8,6 +8,7 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -25,11 +26,45 @@ using namespace zg;
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 8
 #define ZG_NTIMINGS 7
+#define ZG_NSTATS 6
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
+#define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
+
+// Per-device state shared by every context (batch slot) on that GPU: a FIXED pool of stream
+// pairs, created once, and the prepared verifying keys. A context only owns buffers, so a
+// process can hold any number of slots without creating another HIP stream / hardware queue.
+// Why: each hardware queue that dispatches a kernel with a private (scratch) segment keeps a
+// scratch allocation sized for the whole device; the process's scratch pool is bounded, and
+// with a stream pair per context the 7th in-flight context on one GPU pushed it over
+// (HSA_STATUS_ERROR_OUT_OF_RESOURCES from the queue). With the pool, the
+// number of queues -- hence of scratch reservations -- no longer grows with the slots.
+struct zg_dev {
+  int device = 0;
+  int ncu = 0;
+  int refs = 0;
+  std::mutex mu;  // the pool cursor and the VK cache
+  int npairs = 0;
+  hipStream_t main[16] = {}, side[16] = {};
+  hipStream_t hi_main = nullptr, hi_side = nullptr;  // high-priority pair (lazy, zg_set_priority)
+  int next = 0;
+  struct VKEntry {
+    RawVK raw;
+    DevVK* d = nullptr;
+    int err = 0;
+  };
+  std::vector<VKEntry*> vks;  // prepare_verifying_key once per distinct key per device
+};
+
+static std::mutex g_devs_mu;
+static zg_dev* g_devs[64] = {};
+static thread_local std::string g_create_err;
 
 struct zg_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  zg_dev* dev = nullptr;
+  hipStream_t stream = nullptr;  // from the device pool (not owned)
+  hipStream_t side = nullptr;    // VK-side root work, concurrent with the Miller kernels
+  int pair = 0;
   std::mutex mu;
   std::string err;
   uint32_t cap = 0;  // power of two >= max_batch
@@ -37,9 +72,8 @@ struct zg_ctx {
   uint64_t seed = 0;
   int vk_loaded[ZG_NKINDS] = {0, 0, 0};
   int vk_iclen[ZG_NKINDS] = {0, 0, 0};
-  DevVK* d_vk = nullptr;
-  RawVK* d_rawvk = nullptr;
-  int* d_int = nullptr;  // scratch ints
+  DevVK* d_vk = nullptr;  // this slot's 3 kinds (copied from the device cache)
+  int* d_int = nullptr;   // scratch ints: [8] bfail, [9] fused-wait failure
   // batch
   uint8_t *d_proofs = nullptr, *d_kinds = nullptr, *d_inputs = nullptr, *d_ninputs = nullptr, *d_r = nullptr,
           *d_status = nullptr, *d_bytes = nullptr, *d_okbits = nullptr;
@@ -48,6 +82,7 @@ struct zg_ctx {
   int* d_prog = nullptr;  // cap / 64: per lines block, steps published (fused R-chain + f-chain)
   int ncu = 0;            // compute units of the device
   int fuse = -1;          // ZG_LINES_FCHAIN: -1 auto (both grids resident at once), 0 never, 1 always
+  int fuse_off = 0;       // a fused launch ever timed out waiting: split launches from then on
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
@@ -63,10 +98,13 @@ struct zg_ctx {
   int state = 0;
   size_t n = 0, npad = 0;
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
-  hipStream_t side = nullptr;  // VK-side root work, concurrent with the Miller kernel
-  int root_pairs_ready = 0;     // the pipeline already ran the root's MSM + VK pairs on `side`
+  int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
+  int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
+  // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
+  // (bfail, deferred recomputes), [4] bisections, [5] nodes checked by bisection
+  uint64_t stats[ZG_NSTATS] = {};
   uint64_t calls = 0;
 };
 
@@ -82,19 +120,77 @@ static int fail(zg_ctx* c, int code, const std::string& msg) {
 
 static unsigned nblocks(size_t n) { return (unsigned)((n + ZG_BLOCK - 1) / ZG_BLOCK); }
 
-extern "C" const char* zg_version(void) { return "zebra_amd zg 0.1 gfx950"; }
+extern "C" const char* zg_version(void) { return "zebra_amd zg 0.2 gfx950"; }
 
-extern "C" const char* zg_last_error(zg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+extern "C" const char* zg_last_error(zg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
 template <class T>
 static hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, sizeof(T) * (count ? count : 1));
 }
 
+static void dev_release(zg_dev* d) {
+  std::lock_guard<std::mutex> g(g_devs_mu);
+  if (--d->refs > 0) return;
+  hipSetDevice(d->device);
+  for (int i = 0; i < d->npairs; i++) {
+    if (d->main[i]) hipStreamDestroy(d->main[i]);
+    if (d->side[i]) hipStreamDestroy(d->side[i]);
+  }
+  if (d->hi_main) hipStreamDestroy(d->hi_main);
+  if (d->hi_side) hipStreamDestroy(d->hi_side);
+  for (auto* e : d->vks) {
+    if (e->d) hipFree(e->d);
+    delete e;
+  }
+  g_devs[d->device] = nullptr;
+  delete d;
+}
+
+// the device's state, created on first use (streams created here, never per context)
+static zg_dev* dev_acquire(int device, std::string* err) {
+  std::lock_guard<std::mutex> g(g_devs_mu);
+  if (device < 0 || device >= 64) {
+    *err = "bad device ordinal";
+    return nullptr;
+  }
+  zg_dev* d = g_devs[device];
+  if (!d) {
+    d = new zg_dev();
+    d->device = device;
+    int np = ZG_DEFAULT_PAIRS;
+    if (const char* e = getenv("ZG_STREAM_PAIRS")) np = atoi(e);
+    np = np < 1 ? 1 : np > 16 ? 16 : np;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&d->ncu, hipDeviceAttributeMultiprocessorCount, device);
+    for (int i = 0; e == hipSuccess && i < np; i++) {
+      e = hipStreamCreateWithFlags(&d->main[i], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->side[i], hipStreamNonBlocking);
+      if (e == hipSuccess) d->npairs = i + 1;
+    }
+    if (e != hipSuccess) {
+      *err = std::string("device init: ") + hipGetErrorString(e);
+      d->refs = 1;
+      g_devs[device] = d;
+      g_devs_mu.unlock();
+      dev_release(d);
+      g_devs_mu.lock();
+      return nullptr;
+    }
+    g_devs[device] = d;
+  }
+  d->refs++;
+  return d;
+}
+
 extern "C" zg_ctx* zg_create(const zg_config* cfg) {
-  zg_ctx* ctx = new zg_ctx();
   zg_config def = {0, 65536, 0, 0};
   if (!cfg) cfg = &def;
+  g_create_err.clear();
+  zg_dev* dev = dev_acquire(cfg->device, &g_create_err);
+  if (!dev) return nullptr;
+  zg_ctx* ctx = new zg_ctx();
+  ctx->dev = dev;
   ctx->device = cfg->device;
   uint32_t mb = cfg->max_batch ? cfg->max_batch : 65536;
   uint32_t cap = 2;
@@ -102,31 +198,50 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ctx->cap = cap;
   ctx->seeded = cfg->seeded;
   ctx->seed = cfg->seed;
-  bool ok = hipSetDevice(ctx->device) == hipSuccess &&
-            hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) == hipSuccess;
-  ok = ok && hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess;
+  ctx->ncu = dev->ncu;
+  {
+    std::lock_guard<std::mutex> g(dev->mu);
+    ctx->pair = dev->next++ % dev->npairs;
+  }
+  ctx->stream = dev->main[ctx->pair];
+  ctx->side = dev->side[ctx->pair];
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
-  ok = ok && dalloc(&ctx->d_vk, ZG_NKINDS) == hipSuccess && dalloc(&ctx->d_rawvk, 1) == hipSuccess &&
-       dalloc(&ctx->d_int, 16) == hipSuccess;
-  ok = ok && dalloc(&ctx->d_proofs, (size_t)cap * 192) == hipSuccess && dalloc(&ctx->d_kinds, cap) == hipSuccess &&
-       dalloc(&ctx->d_inputs, (size_t)cap * 288) == hipSuccess && dalloc(&ctx->d_ninputs, cap) == hipSuccess &&
-       dalloc(&ctx->d_r, ((size_t)cap + 3) / 4 * 64)  /* whole ChaCha20 blocks */ == hipSuccess && dalloc(&ctx->d_status, cap) == hipSuccess &&
-       dalloc(&ctx->d_okbits, (size_t)cap * 3) == hipSuccess &&
-       dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK) == hipSuccess;
-  ok = ok && dalloc(&ctx->d_ptA, cap) == hipSuccess &&
-       dalloc(&ctx->d_ptAC, 2 * (size_t)cap) == hipSuccess && dalloc(&ctx->d_prog, (size_t)cap / 64 + 1) == hipSuccess && dalloc(&ctx->d_ptB, cap) == hipSuccess &&
-       dalloc(&ctx->d_ftree, 2 * (size_t)cap) == hipSuccess &&
-       dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3) == hipSuccess &&
-       dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS) == hipSuccess &&
-       dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC) == hipSuccess;
-  ok = ok && dalloc(&ctx->d_nodes, ZG_NODE_CHUNK) == hipSuccess &&
-       dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS) == hipSuccess &&
-       dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS) == hipSuccess &&
-       dalloc(&ctx->d_ok, ZG_NODE_CHUNK) == hipSuccess && dalloc(&ctx->d_out, ZG_NODE_CHUNK) == hipSuccess;
-  for (int i = 0; ok && i < ZG_NEV; i++) ok = hipEventCreate(&ctx->ev[i]) == hipSuccess;
-  ok = ok && hipMemset(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS) == hipSuccess;
-  if (!ok) {
+  hipError_t e = hipSetDevice(ctx->device);
+  auto A = [&](hipError_t r) {
+    if (e == hipSuccess) e = r;
+  };
+  A(dalloc(&ctx->d_vk, ZG_NKINDS));
+  A(dalloc(&ctx->d_int, 16));
+  A(dalloc(&ctx->d_proofs, (size_t)cap * 192));
+  A(dalloc(&ctx->d_kinds, cap));
+  A(dalloc(&ctx->d_inputs, (size_t)cap * 288));
+  A(dalloc(&ctx->d_ninputs, cap));
+  A(dalloc(&ctx->d_r, ((size_t)cap + 3) / 4 * 64));  // whole ChaCha20 blocks
+  A(dalloc(&ctx->d_status, cap));
+  A(dalloc(&ctx->d_okbits, (size_t)cap * 3));
+  A(dalloc(&ctx->d_bytes, (size_t)576 * ZG_NODE_CHUNK));
+  A(dalloc(&ctx->d_ptA, cap));
+  A(dalloc(&ctx->d_ptAC, 2 * (size_t)cap));
+  A(dalloc(&ctx->d_prog, (size_t)cap / 64 + 1));
+  A(dalloc(&ctx->d_ptB, cap));
+  A(dalloc(&ctx->d_ftree, 2 * (size_t)cap));
+  A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
+  A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
+  A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
+  A(dalloc(&ctx->d_nodes, ZG_NODE_CHUNK));
+  A(dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS));
+  A(dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS));
+  A(dalloc(&ctx->d_ok, ZG_NODE_CHUNK));
+  A(dalloc(&ctx->d_out, ZG_NODE_CHUNK));
+  for (int i = 0; i < ZG_NEV; i++) A(hipEventCreate(&ctx->ev[i]));
+  // surface a broken device / stream now rather than inside a later batch
+  A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
+  A(hipMemsetAsync(ctx->d_int, 0, sizeof(int) * 16, ctx->side));
+  A(hipStreamSynchronize(ctx->stream));
+  A(hipStreamSynchronize(ctx->side));
+  if (e != hipSuccess) {
+    g_create_err = std::string(e == hipErrorOutOfMemory ? "out of device memory: " : "HIP error: ") +
+                   hipGetErrorString(e);
     zg_destroy(ctx);
     return nullptr;
   }
@@ -136,7 +251,10 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
 extern "C" void zg_destroy(zg_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
-  void* ptrs[] = {ctx->d_vk, ctx->d_rawvk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
+  // the pool's streams outlive the slot: drain this slot's work before its buffers go
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  if (ctx->side) hipStreamSynchronize(ctx->side);
+  void* ptrs[] = {ctx->d_vk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog};
@@ -144,28 +262,56 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
     if (ctx->ev[i]) hipEventDestroy(ctx->ev[i]);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
-  if (ctx->side) hipStreamDestroy(ctx->side);
+  zg_dev* d = ctx->dev;
   delete ctx;
+  if (d) dev_release(d);
 }
 
 // ------------------------------------------------------------------ verifying keys
+// prepare_verifying_key runs once per distinct key per device (k_vk_prepare, one thread,
+// ~140 ms); every further slot that loads the same key gets a device-to-device copy.
 static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
   if (kind < 0 || kind >= ZG_NKINDS) return fail(ctx, ZG_E_INVAL, "bad kind");
   if (raw.n_ic > ZG_MAX_IC) return fail(ctx, ZG_E_INVAL, "ic longer than 10");
+  if (ctx->state) return fail(ctx, ZG_E_STATE, "verifying key load with a batch in flight");
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipMemcpyAsync(ctx->d_rawvk, &raw, sizeof(RawVK), hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(k_vk_prepare, dim3(1), dim3(1), 0, ctx->stream, ctx->d_rawvk, ctx->d_vk + kind, ctx->d_int);
-  HIPCHK(hipGetLastError());
-  int err = 0;
-  HIPCHK(hipMemcpyAsync(&err, ctx->d_int, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  if (err) {
-    int z = 0;
-    hipMemcpy(&ctx->d_vk[kind].loaded, &z, sizeof(int), hipMemcpyHostToDevice);
-    ctx->vk_loaded[kind] = 0;
-    return fail(ctx, ZG_E_VK, "Invalid curve point in verifying key (field " + std::to_string(err) + ")");
+  zg_dev* dev = ctx->dev;
+  zg_dev::VKEntry* ent = nullptr;
+  {
+    std::lock_guard<std::mutex> g(dev->mu);
+    for (auto* e : dev->vks)
+      if (memcmp(&e->raw, &raw, sizeof(RawVK)) == 0) ent = e;
+    if (!ent) {
+      ent = new zg_dev::VKEntry();
+      ent->raw = raw;
+      RawVK* d_raw = nullptr;
+      hipError_t e = hipMalloc(&ent->d, sizeof(DevVK));
+      if (e == hipSuccess) e = hipMalloc(&d_raw, sizeof(RawVK));
+      if (e == hipSuccess) e = hipMemcpyAsync(d_raw, &raw, sizeof(RawVK), hipMemcpyHostToDevice, ctx->stream);
+      if (e == hipSuccess) e = hipMemsetAsync(ent->d, 0, sizeof(DevVK), ctx->stream);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_vk_prepare, dim3(1), dim3(1), 0, ctx->stream, d_raw, ent->d, ctx->d_int);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipMemcpyAsync(&ent->err, ctx->d_int, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+      if (d_raw) hipFree(d_raw);
+      if (e != hipSuccess) {
+        if (ent->d) hipFree(ent->d);
+        delete ent;
+        return fail(ctx, ZG_E_HIP, std::string("prepare_verifying_key: ") + hipGetErrorString(e));
+      }
+      dev->vks.push_back(ent);
+    }
   }
+  if (ent->err) {
+    HIPCHK(hipMemsetAsync(ctx->d_vk + kind, 0, sizeof(DevVK), ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->vk_loaded[kind] = 0;
+    return fail(ctx, ZG_E_VK, "Invalid curve point in verifying key (field " + std::to_string(ent->err) + ")");
+  }
+  HIPCHK(hipMemcpyAsync(ctx->d_vk + kind, ent->d, sizeof(DevVK), hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->vk_loaded[kind] = 1;
   ctx->vk_iclen[kind] = raw.n_ic;
   return ZG_OK;
@@ -449,7 +595,9 @@ static int run_pipeline(zg_ctx* ctx) {
   // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
   const unsigned pgroups = (unsigned)((ctx->npad / 2 + 63) / 64);
-  const bool fused = ctx->fuse == 1 || (ctx->fuse < 0 && groups + pgroups <= (unsigned)ctx->ncu);
+  const bool fused = ctx->fuse == 1 ||
+                     (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu);
+  ctx->fused_last = fused;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
@@ -497,6 +645,7 @@ static int check_kinds(zg_ctx* ctx, size_t n, const uint8_t* kinds) {
 }
 
 static int begin_common(zg_ctx* ctx, size_t n) {
+  if (ctx->state != 0) return fail(ctx, ZG_E_STATE, "zg_batch_begin with a batch in flight (finish it first)");
   if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
   ctx->root_pairs_ready = 0;
   ctx->n = n;
@@ -507,10 +656,10 @@ static int begin_common(zg_ctx* ctx, size_t n) {
   return ZG_OK;
 }
 
-extern "C" int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
+// the *_locked helpers assume ctx->mu is held: zg_verify_batch holds it from begin to finish,
+// so no other thread can begin a batch on the same context in between
+static int batch_begin_locked(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
                               const uint8_t* inputs, const uint8_t* n_inputs, const uint8_t* r) {
-  if (!ctx || (n && (!proofs || !kinds || !inputs))) return ZG_E_INVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   int rc = begin_common(ctx, n);
   if (rc) return rc;
@@ -529,6 +678,13 @@ extern "C" int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, cons
   if ((rc = run_pipeline(ctx))) return rc;
   ctx->state = 1;
   return ZG_OK;
+}
+
+extern "C" int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
+                              const uint8_t* inputs, const uint8_t* n_inputs, const uint8_t* r) {
+  if (!ctx || (n && (!proofs || !kinds || !inputs))) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return batch_begin_locked(ctx, n, proofs, kinds, inputs, n_inputs, r);
 }
 
 extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,
@@ -595,15 +751,21 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
   return ZG_OK;
 }
 
-extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
-  if (!ctx || !partial) return ZG_E_INVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_partial before zg_batch_begin");
-  HIPCHK(hipSetDevice(ctx->device));
-  std::vector<int> root = {1};
-  int rc = check_nodes(ctx, root, 1, nullptr, partial);
+// after the batch's device work: timings and the pipeline's flags (B subgroup failures that
+// forced the gated recompute; a fused launch whose consumers timed out waiting, which turns
+// the fused shape off for this context)
+static int collect_batch_stats(zg_ctx* ctx) {
+  int flags[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(flags, ctx->d_int + 8, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
+  ctx->stats[0]++;
+  if (ctx->fused_last) ctx->stats[1]++;
+  if (flags[1]) {
+    ctx->stats[2]++;
+    ctx->fuse_off = 1;
+  }
+  if (flags[0]) ctx->stats[3]++;
   hipEventElapsedTime(&ctx->timings[0], ctx->ev[0], ctx->ev[1]);  // decode
   hipEventElapsedTime(&ctx->timings[1], ctx->ev[1], ctx->ev[7]);  // lines (R-chain)
   hipEventElapsedTime(&ctx->timings[2], ctx->ev[7], ctx->ev[2]);  // f-chain
@@ -611,7 +773,18 @@ extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
   hipEventElapsedTime(&ctx->timings[4], ctx->ev[3], ctx->ev[4]);  // root partial (after the side stream)
   hipEventElapsedTime(&ctx->timings[5], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
   hipEventElapsedTime(&ctx->timings[6], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
-  return rc;
+  return ZG_OK;
+}
+
+extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
+  if (!ctx || !partial) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_partial before zg_batch_begin");
+  HIPCHK(hipSetDevice(ctx->device));
+  std::vector<int> root = {1};
+  int rc = check_nodes(ctx, root, 1, nullptr, partial);
+  if (rc) return rc;
+  return collect_batch_stats(ctx);
 }
 
 extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok) {
@@ -630,21 +803,30 @@ extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, i
   return ZG_OK;
 }
 
+// Moves the context to the device's high-priority stream pair (created once per device) or
+// back to its pool pair. No stream is created or destroyed per context.
 extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
   if (!ctx) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   if (ctx->state != 0) return fail(ctx, ZG_E_STATE, "zg_set_priority with a batch in flight");
   HIPCHK(hipSetDevice(ctx->device));
-  int lo = 0, hi = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->side));
-  HIPCHK(hipStreamDestroy(ctx->stream));
-  HIPCHK(hipStreamDestroy(ctx->side));
-  ctx->stream = ctx->side = nullptr;
-  const int prio = high ? hi : lo;  // numerically lower = higher priority (hi <= lo)
-  HIPCHK(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio));
-  HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio));
+  zg_dev* d = ctx->dev;
+  if (high) {
+    std::lock_guard<std::mutex> gd(d->mu);
+    if (!d->hi_main) {
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));  // numerically lower = higher priority
+      HIPCHK(hipStreamCreateWithPriority(&d->hi_main, hipStreamNonBlocking, hi));
+      HIPCHK(hipStreamCreateWithPriority(&d->hi_side, hipStreamNonBlocking, hi));
+    }
+    ctx->stream = d->hi_main;
+    ctx->side = d->hi_side;
+  } else {
+    ctx->stream = d->main[ctx->pair];
+    ctx->side = d->side[ctx->pair];
+  }
   return ZG_OK;
 }
 
@@ -653,8 +835,10 @@ extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
 static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
   std::vector<int> level = {1};
   const int npad = (int)ctx->npad, n = (int)ctx->n;
+  ctx->stats[4]++;
   while (!level.empty()) {
     std::vector<int> ok;
+    ctx->stats[5] += level.size();
     int rc = check_nodes(ctx, level, 0, &ok, nullptr);
     if (rc) return rc;
     std::vector<int> next;
@@ -668,12 +852,8 @@ static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
       }
       // children that start at or beyond n hold only padding (identity): skip them
       for (int c = 2 * node; c <= 2 * node + 1; c++) {
-        int depth_span = 1;
         int x = c;
-        while (x < npad) {
-          x <<= 1;
-          depth_span <<= 1;
-        }
+        while (x < npad) x <<= 1;
         int first = x - npad;
         if (first < n) next.push_back(c);
       }
@@ -683,9 +863,7 @@ static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
   return ZG_OK;
 }
 
-extern "C" int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status) {
-  if (!ctx || !status) return ZG_E_INVAL;
-  std::lock_guard<std::mutex> g(ctx->mu);
+static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status) {
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_finish before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
   std::vector<uint8_t> st(ctx->n);
@@ -693,33 +871,51 @@ extern "C" int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (!batch_ok) {
     int rc = bisect(ctx, st);
-    if (rc) return rc;
+    if (rc) {
+      ctx->state = 0;  // the batch is abandoned; the context stays usable
+      return rc;
+    }
   }
   for (size_t i = 0; i < ctx->n; i++) status[i] = st[i] == ST_PENDING ? ST_OK : st[i];
   ctx->state = 0;
   return ZG_OK;
 }
 
+extern "C" int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status) {
+  if (!ctx || (!status && ctx->n)) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return batch_finish_locked(ctx, batch_ok, status);
+}
+
 extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds,
                                const uint8_t* inputs, const uint8_t* n_inputs, const uint8_t* r, uint8_t* status,
                                uint8_t* gt_out) {
-  if (!ctx || !status) return ZG_E_INVAL;
-  int rc = zg_batch_begin(ctx, n, proofs, kinds, inputs, n_inputs, r);
+  if (!ctx || !status || (n && (!proofs || !kinds || !inputs))) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  int rc = batch_begin_locked(ctx, n, proofs, kinds, inputs, n_inputs, r);
   if (rc) return rc;
-  int ok = 1;
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    std::vector<int> root = {1}, okv;
-    if (gt_out && (rc = check_nodes(ctx, root, 2, nullptr, gt_out))) return rc;
-    if ((rc = check_nodes(ctx, root, 0, &okv, nullptr))) return rc;
-    ok = okv[0];
+  std::vector<int> root = {1}, okv;
+  if (gt_out) rc = check_nodes(ctx, root, 2, nullptr, gt_out);
+  if (!rc) rc = check_nodes(ctx, root, 0, &okv, nullptr);
+  if (!rc) rc = collect_batch_stats(ctx);
+  if (rc) {
+    ctx->state = 0;
+    return rc;
   }
-  return zg_batch_finish(ctx, ok, status);
+  return batch_finish_locked(ctx, okv[0], status);
 }
 
 extern "C" int zg_last_timings(zg_ctx* ctx, float* ms7) {
   if (!ctx || !ms7) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
   for (int i = 0; i < ZG_NTIMINGS; i++) ms7[i] = ctx->timings[i];
+  return ZG_OK;
+}
+
+extern "C" int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n) {
+  if (!ctx || (n && !out)) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (size_t i = 0; i < n; i++) out[i] = i < ZG_NSTATS ? ctx->stats[i] : 0;
   return ZG_OK;
 }
 
@@ -833,20 +1029,39 @@ extern "C" int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* sr
   return rc;
 }
 
-extern "C" int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s) {
+extern "C" int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s) { return zg_bench_mad_rate_clock(ctx, macs_per_s, nullptr); }
+
+extern "C" int zg_bench_mad_rate_clock(zg_ctx* ctx, double* macs_per_s, double* clock_hz) {
   if (!ctx || !macs_per_s) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   const int blocks = 256 * 16, threads = 256, iters = 2048;
-  hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, 16, 1u);
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, iters, 1u);
-  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  HIPCHK(hipEventSynchronize(ctx->ev[1]));
+  uint64_t* d_st = nullptr;
+  HIPCHK(hipMalloc(&d_st, sizeof(uint64_t) * 2 * blocks));
+  hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, 16, 1u,
+                     (uint64_t*)nullptr);
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipEventRecord(ctx->ev[0], ctx->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_mad_rate, dim3(blocks), dim3(threads), 0, ctx->stream, (uint64_t*)ctx->d_int, iters, 1u,
+                       d_st);
+    e = hipEventRecord(ctx->ev[1], ctx->stream);
+  }
+  if (e == hipSuccess) e = hipEventSynchronize(ctx->ev[1]);
   float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+  std::vector<uint64_t> st(2 * blocks);
+  if (e == hipSuccess) e = hipMemcpy(st.data(), d_st, sizeof(uint64_t) * 2 * blocks, hipMemcpyDeviceToHost);
+  hipFree(d_st);
+  if (e != hipSuccess) return fail(ctx, ZG_E_HIP, std::string("mad rate probe: ") + hipGetErrorString(e));
   *macs_per_s = (double)blocks * threads * iters * 64.0 / (ms * 1e-3);
+  if (clock_hz) {  // median over blocks of shader ticks / (constant ticks / 100 MHz)
+    std::vector<double> hz;
+    for (int i = 0; i < blocks; i++)
+      if (st[2 * i + 1]) hz.push_back((double)st[2 * i] / ((double)st[2 * i + 1] / 100e6));
+    std::sort(hz.begin(), hz.end());
+    *clock_hz = hz.empty() ? 0.0 : hz[hz.size() / 2];
+  }
   return ZG_OK;
 }
 

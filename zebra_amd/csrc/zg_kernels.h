@@ -527,12 +527,15 @@ __global__ void __launch_bounds__(64) k_rerandomize(const DevVK* vks, const uint
 }
 
 // v_mad_u64_u32 throughput probe: 8 independent 64-bit accumulator chains per lane,
-// 64 MACs per chain per iteration
-__global__ void __launch_bounds__(256) k_mad_rate(uint64_t* sink, int iters, uint32_t seed) {
+// 64 MACs per chain per iteration. stamps (optional): per block, the shader-clock ticks
+// (s_memtime) and the 100 MHz constant-clock ticks (s_memrealtime) around the loop, so the
+// host can state the clock the probe ran at (MI355X_MICROARCH.md, DVFS give-back item 6).
+__global__ void __launch_bounds__(256) k_mad_rate(uint64_t* sink, int iters, uint32_t seed, uint64_t* stamps) {
   uint32_t a = seed + threadIdx.x, b = seed * 3 + blockIdx.x;
   uint64_t c[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) c[q] = a + q * b;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; it++) {
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -543,6 +546,11 @@ __global__ void __launch_bounds__(256) k_mad_rate(uint64_t* sink, int iters, uin
   uint64_t x = 0;
 #pragma unroll
   for (int q = 0; q < 8; q++) x ^= c[q];
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (stamps && threadIdx.x == 0) {
+    stamps[2 * blockIdx.x] = t1 - t0 + (x == 0x123456789ull);
+    stamps[2 * blockIdx.x + 1] = r1 - r0;
+  }
   if (x == 0x123456789ull) sink[0] = x;
 }
 

@@ -57,7 +57,9 @@ def lib():
         L.zg_batch_finish.argtypes = [vp, i, u8p]
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
         L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        L.zg_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz]
         L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.zg_bench_mad_rate_clock.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.zg_chacha20_blocks.argtypes = [vp, u8p, u8p, ctypes.c_uint32, ctypes.c_size_t, u8p]
         L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
         L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
@@ -136,7 +138,7 @@ class Context:
         cfg = _Config(device, max_batch, 1 if seed is not None else 0, seed or 0)
         self._p = L.zg_create(ctypes.byref(cfg))
         if not self._p:
-            raise ZgError(-2, "zg_create failed (no GPU / HIP error)")
+            raise ZgError(-2, "zg_create failed: %s" % (L.zg_last_error(None) or b"no GPU / HIP error").decode())
         if load_builtin:
             for k in (KIND_SPEND, KIND_OUTPUT, KIND_SPROUT):
                 self.vk_load_builtin(k)
@@ -237,6 +239,15 @@ class Context:
         self._chk(lib().zg_last_timings(self._p, a))
         return list(a)
 
+    STAT_NAMES = ("batches", "fused_launches", "fused_wait_failures", "b_subgroup_recomputes", "bisections",
+                  "bisect_nodes")
+
+    def stats(self):
+        """cumulative counters (include/zg.h zg_stats) as a dict"""
+        a = (ctypes.c_uint64 * len(self.STAT_NAMES))()
+        self._chk(lib().zg_stats(self._p, a, len(self.STAT_NAMES)))
+        return dict(zip(self.STAT_NAMES, list(a)))
+
     def synth_rerandomize(self, src_proofs, src_kinds, src_index, seed):
         n = len(src_index)
         idx = (ctypes.c_uint32 * max(n, 1))(*src_index)
@@ -252,7 +263,8 @@ class Context:
         self._chk(lib().zg_chacha20_blocks(self._p, bytes(key), bytes(nonce), counter, nblocks, out))
         return out.raw[:64 * nblocks]
 
-    def bench_mad_rate(self):
-        v = ctypes.c_double(0)
-        self._chk(lib().zg_bench_mad_rate(self._p, ctypes.byref(v)))
-        return v.value
+    def bench_mad_rate(self, with_clock=False):
+        """v_mad_u64_u32 MACs/s of the probe; with_clock: (rate, shader clock in Hz)"""
+        v, hz = ctypes.c_double(0), ctypes.c_double(0)
+        self._chk(lib().zg_bench_mad_rate_clock(self._p, ctypes.byref(v), ctypes.byref(hz)))
+        return (v.value, hz.value) if with_clock else v.value
