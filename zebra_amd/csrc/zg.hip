@@ -17,6 +17,7 @@
 #include "zg_blake2b.h"
 #include "zg_chacha.h"
 #include "zg_kernels.h"
+#include "zg_msm.h"
 #include "zg_prep.h"
 #include "zg_vk_embed.h"  // generated from zebra_amd/res/*.json by zebra_amd/build.py
 
@@ -88,6 +89,8 @@ struct zg_ctx {
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
   G1J* d_ctree = nullptr;
   Fr* d_stree = nullptr;
+  MsmBufs msm = {};       // K4: Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)
+  int trees_built = 0;    // the full C / Fr trees exist for this batch (bisection only)
   // node checks
   int* d_nodes = nullptr;
   G1J* d_msm = nullptr;
@@ -228,6 +231,13 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
   A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
   A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
+  A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT));
+  A(dalloc(&ctx->msm.start, ZG_MSM_NCOUNT + 1));
+  A(dalloc(&ctx->msm.cursor, ZG_MSM_NCOUNT));
+  A(dalloc(&ctx->msm.entries, 2 * (size_t)cap * ZG_MSM_W));
+  A(dalloc(&ctx->msm.bsum, (size_t)ZG_MSM_NCOUNT * ZG_MSM_PARTS));
+  A(dalloc(&ctx->msm.wsum, ZG_MSM_GROUPS));
+  A(dalloc(&ctx->msm.frpart, ((size_t)cap / ZG_FR_CHUNK + 1) * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->d_nodes, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS));
   A(dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS));
@@ -237,6 +247,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   // surface a broken device / stream now rather than inside a later batch
   A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
   A(hipMemsetAsync(ctx->d_int, 0, sizeof(int) * 16, ctx->side));
+  A(hipMemsetAsync(ctx->msm.entries, 0, sizeof(uint32_t) * 2 * (size_t)cap * ZG_MSM_W, ctx->side));
   A(hipStreamSynchronize(ctx->stream));
   A(hipStreamSynchronize(ctx->side));
   if (e != hipSuccess) {
@@ -257,7 +268,8 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   void* ptrs[] = {ctx->d_vk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
-                  ctx->d_okbits, ctx->d_ptAC, ctx->d_prog};
+                  ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
+                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -560,13 +572,16 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
   return ZG_OK;
 }
 
-namespace zg {  // zg_decode.hip
-hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);
+namespace zg {
+hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);          // zg_decode.hip
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate);  // zg_msm.hip
+hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
 }
 
 // The pipeline on device-resident inputs already in ctx buffers.
 //   main stream: decode -> R-chain (lines + G2 subgroup checks) -> f-chain -> Fq12 product tree
-//   side stream: (after decode) C / Fr sum trees -> root VK-side MSM -> root VK Miller loops
+//   side stream: (after decode) K4 Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)
+//                -> root VK-side MSM -> root VK Miller loops
 // The side stream only needs the decode results, so its few-thread work overlaps the lines
 // and f-chain kernels instead of extending the critical path. A B_i that fails its G2
 // subgroup check in k_batch_lines (invalid proofs only) counts in bfail, and the side-stream
@@ -583,10 +598,8 @@ static int run_pipeline(zg_ctx* ctx) {
   // side stream
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->side));
-  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo, (const int*)nullptr);
-    HIPCHK(hipGetLastError());
-  }
+  ctx->trees_built = 0;
+  HIPCHK(launch_msm_root(ctx->side, b, ctx->msm, nullptr));
   NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
   int rc = launch_node_msm_pairs(ctx, b, nb, ctx->side);
   if (rc) return rc;
@@ -624,11 +637,7 @@ static int run_pipeline(zg_ctx* ctx) {
   }
   HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream trees + root pairs complete
   // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
-  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo,
-                       (const int*)b.bfail);
-    HIPCHK(hipGetLastError());
-  }
+  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail));
   rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
   if (rc) return rc;
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
@@ -832,10 +841,26 @@ extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
 
 // Bisection over the product trees: a failing node's children are re-checked exactly;
 // a failing leaf is a proof whose own check fails (r_i != 0 makes it bellman's check).
+// bisection needs every node's C and Fr sums: the per-proof r_i C_i (GLV) leaves and the full
+// trees, built only now (a valid batch never needs them: K4 forms the root directly)
+static int build_trees(zg_ctx* ctx) {
+  if (ctx->trees_built) return ZG_OK;
+  BatchBufs b = batch_bufs(ctx);
+  HIPCHK(launch_c_leaves(ctx->stream, b));
+  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
+    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo, (const int*)nullptr);
+    HIPCHK(hipGetLastError());
+  }
+  ctx->trees_built = 1;
+  return ZG_OK;
+}
+
 static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
   std::vector<int> level = {1};
   const int npad = (int)ctx->npad, n = (int)ctx->n;
   ctx->stats[4]++;
+  int rc0 = build_trees(ctx);
+  if (rc0) return rc0;
   while (!level.empty()) {
     std::vector<int> ok;
     ctx->stats[5] += level.size();

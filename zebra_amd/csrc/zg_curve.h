@@ -110,6 +110,33 @@ ZG_INL Jac<F> jac_add_inl(const Jac<F>& p, const Jac<F>& q) {
   return {X3, Y3, Z3};
 }
 
+// the same with the doubling case inlined too (no out-of-line call with pointers to the
+// caller's frame: kernels that must not touch scratch)
+template <class F>
+ZG_INL Jac<F> jac_add_full(const Jac<F>& p, const Jac<F>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  F Z1Z1 = F_sqr(p.z);
+  F Z2Z2 = F_sqr(q.z);
+  F U1 = F_mul(p.x, Z2Z2);
+  F U2 = F_mul(q.x, Z1Z1);
+  F S1 = F_mul(F_mul(p.y, q.z), Z2Z2);
+  F S2 = F_mul(F_mul(q.y, p.z), Z1Z1);
+  F H = F_sub(U2, U1);
+  F rr = F_dbl(F_sub(S2, S1));
+  if (F_is_zero(H)) {
+    if (F_is_zero(rr)) return jac_dbl_inl(p);
+    return jac_infinity<F>();
+  }
+  F I = F_sqr(F_dbl(H));
+  F J = F_mul(H, I);
+  F V = F_mul(U1, I);
+  F X3 = F_sub(F_sub(F_sqr(rr), J), F_dbl(V));
+  F Y3 = F_sub(F_mul(rr, F_sub(V, X3)), F_dbl(F_mul(S1, J)));
+  F Z3 = F_mul(F_sub(F_sub(F_sqr(F_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return {X3, Y3, Z3};
+}
+
 template <class F>
 ZG_NOINL void jac_add_p(Jac<F>* r, const Jac<F>* p, const Jac<F>* q) { *r = jac_add_inl(*p, *q); }
 template <class F>

@@ -14,15 +14,13 @@ namespace zg {
 // point goes to ptAC (inf = the point did not decode).
 //
 // k_decode_points: one wave per (64 proofs, job), the jobs of a decoded point being independent
-// of each other: blocks [0, 2G) alternate the GLV products [r_i] A_i (to affine -> ptA) and
-// [r_i] C_i (Jacobian -> the proof's ctree leaf of its kind); blocks [2G, 4G) alternate the G1
-// subgroup checks of A and C (sigma(P) = -[x^2] P -> okbits); blocks [4G, 5G) decompress B (Fq2
-// sqrt; its G2 subgroup check rides on k_batch_lines). Splitting the subgroup check off the
-// scalar product takes ~40 % off the longest chain a wave runs, which is what a small shard
-// (an 8,192-proof rank of the 8-GPU run: 640 waves on 1,024 SIMDs) waits for; the total work
-// is unchanged. The heavy waves are dispatched first, two per SIMD (ZG_DECODE_WPE), and the B
-// waves fill the tail. The scalar products run before the statuses are known (a point that did
-// not decode skips its own; the rest are masked by k_decode_finish).
+// of each other: blocks [0, G) the GLV products [r_i] A_i (to affine -> ptA); blocks [G, 3G)
+// alternate the G1 subgroup checks of A and C (sigma(P) = -[x^2] P -> okbits); blocks
+// [3G, 4G) decompress B (Fq2 sqrt; its G2 subgroup check rides on k_batch_lines). C needs no
+// per-proof scalar product: sum r_i C_i is K4's Pippenger MSM (zg_msm.h) on the side stream.
+// The heavy waves are dispatched first, two per SIMD (ZG_DECODE_WPE), and the B waves fill the
+// tail. The scalar products run before the statuses are known (a point that did not decode
+// skips its own; the rest are masked by k_decode_finish).
 __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) {
   const int role = blockIdx.x & 1;  // 0 A, 1 C (wave-uniform)
   const int i = (blockIdx.x >> 1) * 64 + (threadIdx.x & 63);
@@ -37,12 +35,11 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) 
 __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b) {
   const int G = (b.npad + 63) / 64;
   const int blk = blockIdx.x;
-  const int job = blk < 2 * G ? 0 : blk < 4 * G ? 1 : 2;  // 0 GLV, 1 subgroup, 2 B (wave-uniform)
-  const int role = job == 2 ? 2 : (blk & 1);             // 0 A, 1 C, 2 B
-  const int grp = job == 2 ? blk - 4 * G : (blk - 2 * G * job) >> 1;
+  const int job = blk < G ? 0 : blk < 3 * G ? 1 : 2;  // 0 GLV A, 1 subgroup, 2 B (wave-uniform)
+  const int role = job == 0 ? 0 : job == 2 ? 2 : ((blk - G) & 1);  // 0 A, 1 C, 2 B
+  const int grp = job == 0 ? blk : job == 2 ? blk - 3 * G : (blk - G) >> 1;
   const int i = grp * 64 + (threadIdx.x & 63);
   if (i >= b.npad) return;
-  const int leaf = b.npad + i;
   if (job == 2) {
     G2A q;
     q.inf = true;
@@ -60,19 +57,15 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b
   }
   uint64_t ra = 0, rb = 0;
   if (ok) batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
-  if (role == 0) {
-    G1A o;
-    o.inf = true;
-    if (ok) o = jac_to_aff(g1_glv_mul(p, ra, rb));
-    b.ptA[i] = o;
-  } else if (ok) {
-    b.ctree[leaf * ZG_NKINDS + b.kinds[i]] = g1_glv_mul(p, ra, rb);
-  }
+  G1A o;
+  o.inf = true;
+  if (ok) o = jac_to_aff(g1_glv_mul(p, ra, rb));
+  b.ptA[i] = o;
 }
 
 // k_decode_finish: lane = proof. bellman's precedence (sapling.rs:157-167): input canonicity,
 // Proof::read, input count; statuses; masks the point results of proofs that are not pending;
-// the Fr leaves r_i, r_i x_ij of its kind, the other kinds' leaves zero / infinity.
+// the Fr leaves r_i, r_i x_ij of its kind, the other kinds' leaves zero.
 __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   if (i >= b.npad) return;
@@ -99,7 +92,6 @@ __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
   // B still owes its subgroup check (k_batch_lines) if Proof::read got that far
   b.ptB[i].inf = !(live && (st == ST_PENDING || st == ST_MALFORMED_VK));
   for (int kd = 0; kd < ZG_NKINDS; kd++) {
-    if (kd != kind || !pend) b.ctree[leaf * ZG_NKINDS + kd] = jac_infinity<Fq>();
     Fr* s = b.stree + (leaf * ZG_NKINDS + kd) * ZG_MAX_IC;
     for (int m = 0; m < ZG_MAX_IC; m++) s[m] = fp_zero<FrM>();
   }

@@ -10,10 +10,10 @@
 
 namespace zg {
 
-// G1 square roots, then the point jobs (GLV products, subgroup checks, B), then per-proof statuses and leaves
+// G1 square roots, then the point jobs (GLV r_i A_i, subgroup checks, B), then per-proof statuses and Fr leaves
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b) {
   hipLaunchKernelGGL(k_decode_sqrt, dim3(2 * groups), dim3(64), 0, st, b);
-  hipLaunchKernelGGL(k_decode_points, dim3(5 * groups), dim3(64), 0, st, b);
+  hipLaunchKernelGGL(k_decode_points, dim3(4 * groups), dim3(64), 0, st, b);
   hipLaunchKernelGGL(k_decode_finish, dim3(groups), dim3(64), 0, st, b);
   return hipGetLastError();
 }

@@ -101,7 +101,6 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
       atomicAdd(b.bfail, 1);
       b.status[proof] = ST_DECODE_INVALID;
       const int leaf = b.npad + proof, kind = b.kinds[proof];
-      b.ctree[leaf * ZG_NKINDS + kind] = jac_infinity<Fq>();
       for (int m = 0; m < ZG_MAX_IC; m++) b.stree[(leaf * ZG_NKINDS + kind) * ZG_MAX_IC + m] = fp_zero<FrM>();
     }
   }
