@@ -30,12 +30,17 @@ sys.path.insert(0, ROOT)
 
 # frozen algorithmic work per proof (Fq-mul-equivalents), attributed to the
 # kernel that performs it (the G2 subgroup check of B rides on the R-chain kernel).
-W_DECODE = 2679 + 2 * 507 + 1593 + 264 + 3   # point decode (2 Fq + 1 Fq2 sqrt), 2 G1 checks, r_i A_i, MSM share, Fr
+W_DECODE = 2679 + 2 * 507 + 1593 + 3         # point decode (2 Fq + 1 Fq2 sqrt), 2 G1 checks, r_i A_i, Fr
+W_K4 = 264                                   # Pippenger sum r_i C_i share (K4, side stream)
 W_LINES = 1634 + 1189                        # G2 line coefficients (R-chain) + G2 subgroup check
 W_FCHAIN = 5192                              # Miller f-chain (sparse line products + squarings)
 W_TREE = 54                                  # tree-product Fq12 multiply
 W_TOTAL = 13622
-assert W_DECODE + W_LINES + W_FCHAIN + W_TREE == W_TOTAL
+assert W_DECODE + W_K4 + W_LINES + W_FCHAIN + W_TREE == W_TOTAL
+# K4 bucket phase, algorithmic HBM bytes: per entry the 4-byte bucket entry and the 100-byte
+# affine C_i it names (G1A), plus the partial bucket sums written once (Jacobian, 144 B)
+K4_ENTRY_BYTES = 4 + 100
+K4_BSUM_BYTES = 3 * 6 * 1024 * 4 * 144
 NOMINAL_LANES = 256 * 4 * 16                        # MI355X: CUs x SIMDs x lanes per clock
 MACS_PER_FQMUL = 288                                # 2 * 12^2 32x32->64 MACs (product + CIOS reduction)
 
@@ -329,19 +334,29 @@ def main():
     if vtime:   # deferred verdicts: the worker thread's time per batch (overlaps the next batches)
         host_ms[1] = 1e3 * sum(vtime) / len(vtime)
     # isolated launches (one batch in flight, after the timed region): the kernels' own roofline
-    iso = []
-    for _ in range(0 if args.no_iso else 3):
-        launch(ctx)
-        ok_, sts_ = complete(ctx)
-        iso.append(timings.pop())
-        assert ok_ and all(x == 0 for x in sts_)
+    # (ZG_SERIAL_SIDE: this context runs the side-stream work -- K4 and the root's VK pairs -- on
+    # its main stream after the product tree, so the Miller kernels are alone on the device)
+    iso, k4_entries = [], None
+    if not args.no_iso:
+        os.environ["ZG_SERIAL_SIDE"] = "1"
+        try:
+            ictx = Context(device=local, max_batch=shard)
+        finally:
+            del os.environ["ZG_SERIAL_SIDE"]
+        for _ in range(3):
+            launch(ictx)
+            ok_, sts_ = complete(ictx)
+            iso.append(timings.pop())
+            assert ok_ and all(x == 0 for x in sts_)
+        k4_entries = ictx.stats()["k4_entries"]
+        ictx.close()
 
     total = shard * world
     value = total * args.steps / dt
-    names = ["decode", "k_batch_lines", "k_batch_fchain", "k_tree_f", "root_partial", "side_stream_vk",
-             "device_pipeline"]
+    names = list(Context.PHASES)
+    NP = len(names)
     # phases = HIP events around launch groups; decode = k_decode_sqrt + k_decode_points + k_decode_finish
-    avg = [sum(t[i] for t in timings) / len(timings) for i in range(7)]
+    avg = [sum(t[i] for t in timings) / len(timings) for i in range(NP)]
     # roofline of the dominant single kernel: the f-chain (the R-chain + f-chain launch when the
     # shard runs them fused -- its lines phase is then empty), algorithmic MACs per launch over
     # its mean launch duration (HIP events, timed region; with batches in flight a launch shares
@@ -351,14 +366,25 @@ def main():
     fused = iso[0][1] < 0.05   # the fused launch leaves the lines phase empty (isolated pass)
     rk, wk = ("k_lines_fchain", W_LINES + W_FCHAIN) if fused else ("k_batch_fchain", W_FCHAIN)
     achieved = wk * MACS_PER_FQMUL * shard / (avg[2] * 1e-3)
-    iso_avg = [sum(t[i] for t in iso) / len(iso) for i in range(7)]
+    iso_avg = [sum(t[i] for t in iso) / len(iso) for i in range(NP)]
     iso_achieved = wk * MACS_PER_FQMUL * shard / (iso_avg[2] * 1e-3)
     phase_frac = {names[i]: w * MACS_PER_FQMUL * shard / (iso_avg[i] * 1e-3) / peak
-                  for i, w in ((0, W_DECODE), (1, W_LINES), (2, W_FCHAIN)) if iso_avg[i] >= 0.05}
-    traffic = None
+                  for i, w in ((0, W_DECODE), (1, W_LINES), (2, W_FCHAIN), (7, W_K4)) if iso_avg[i] >= 0.05}
+    traffic = k4_traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc) and shard == 65536 and not fused:   # the PMC passes run the default 64k bench
-        traffic = json.load(open(pmc)).get(rk)
+        pt = json.load(open(pmc))
+        traffic, k4_traffic = pt.get(rk), pt.get("k_msm_bucket")
+    k4 = None
+    if k4_entries is not None and iso_avg[8] > 0:
+        k4_bytes = k4_entries * K4_ENTRY_BYTES + K4_BSUM_BYTES
+        k4 = {"kernel": "k_msm_bucket", "bound": "hbm", "entries": k4_entries, "algorithmic_bytes": k4_bytes,
+              "ms": iso_avg[8], "achieved_gbs": k4_bytes / (iso_avg[8] * 1e-3) / 1e9, "peak_gbs": 8000.0,
+              "frac": k4_bytes / (iso_avg[8] * 1e-3) / 8e12, "traffic": k4_traffic,
+              "k4_total_ms": iso_avg[7],
+              "note": "HBM GB/s of the Pippenger bucket phase (isolated pass, HIP events around "
+                      "k_msm_bucket): entries x (4-B entry + 100-B affine C_i) + partial sums written; "
+                      "the phase is VALU-bound (mixed additions), not HBM-bound"}
     out = {
         "metric": "Sapling Groth16 proofs verified/sec (batch 64k) at 1/2/4/8 MI355X",
         "value": value, "unit": "proofs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -382,10 +408,12 @@ def main():
                                             "256 CU x 4 SIMD x 16 lanes x 2.4 GHz, one MAC per lane per clock"},
                      "phase_ms": dict(zip(names, iso_avg)), "phase_frac": phase_frac,
                      "note": "no isolated pass (--no-iso): same launches as roofline_inflight" if args.no_iso else
-                             "3 batches with one in flight after the timed region: the kernels alone on the GPU"},
+                             "3 batches with one in flight after the timed region, side-stream work serialised "
+                             "after the product tree (ZG_SERIAL_SIDE): the kernels alone on the GPU"},
         "roofline_inflight": {"kernel": rk, "achieved": achieved / 1e12, "frac": achieved / peak,
                               "kernel_ms": avg[2], "note": "mean launch duration inside the timed region, "
                               "sharing the GPU with the other batches in flight"},
+        "k4_msm_bucket_phase": k4,
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
         "host_ms_per_batch": {"wait_partial": host_ms[0], "exchange_and_final_exp": host_ms[1],

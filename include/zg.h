@@ -182,15 +182,21 @@ int zg_synth_rerandomize(zg_ctx* ctx, size_t n_src, const uint8_t* src_proofs, c
 /* ---- measurement helpers */
 /* time (ms, HIP events on the context streams) of the most recent zg_batch_begin* +
  * zg_batch_partial: [0] decode (main stream), [1] R-chain / line coefficients (+ G2 subgroup
- * checks), [2] f-chain (per-proof Miller values), [3] Fq12 product tree, [4] root partial,
- * [5] side stream (C/Fr trees + VK-side MSM + VK Miller loops, overlapping [2]-[3]),
+ * checks), [2] f-chain (per-proof Miller values), [3] Fq12 product tree, [4] root partial
+ * (waiting for the side stream, gated recompute, root product), [5] side stream (K4 Pippenger
+ * sum r_i C_i + root Fr sums + VK-side MSM + VK Miller loops, overlapping [1]-[3]; with
+ * ZG_SERIAL_SIDE=1 in the environment at zg_create it runs on the main stream after [3]),
  * [6] whole device pipeline */
 int zg_last_timings(zg_ctx* ctx, float* ms7);
+/* the same, n values: [0]-[6] as above, [7] K4 (the Pippenger MSM + root Fr sums, part of [5]),
+ * [8] K4's bucket phase (k_msm_bucket alone). Writes min(n, 9) values, zero beyond. */
+int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
 /* cumulative counters of this context: [0] batches, [1] fused R-chain + f-chain launches,
  * [2] fused launches whose consumers timed out waiting (the f-chain was recomputed by the
  * split kernel; the context uses split launches from then on), [3] batches with a B that
  * failed its G2 subgroup check (gated recompute of the VK-side root work), [4] bisections,
- * [5] tree nodes checked by bisection. Writes min(n, 6) values, zero beyond. */
+ * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
+ * non-zero window digit, summed over the windows). Writes min(n, 7) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

@@ -1,0 +1,186 @@
+//! verification/src/gpu/collect.rs -- block-level Groth16 collection with the reference's error
+//! precedence (a transcription of zebra_amd/collector.py).
+//!
+//!   ChainAcceptor::check_transactions  verification/src/accept_chain.rs:76-81
+//!       the LOWEST failing tx index wins (rayon fold/reduce)
+//!   TransactionAcceptor::check         verification/src/accept_transaction.rs:68-84
+//!       ... -> eval -> join_split.check -> sapling.check
+//!   JoinSplitVerification::check       accept_transaction.rs:649-657
+//!       ed25519 sig -> per description: proof (InvalidJoinSplit(i)), tree root -> nullifiers
+//!   SaplingVerification                accept_transaction.rs:700-714
+//!       per spend (prep, spend_auth_sig, proof), per output (prep, proof), binding sig
+//!       -> InvalidSapling; then nullifiers
+//!
+//! The checks that are not Groth16 are evaluated by the caller as today and handed in as
+//! outcomes; every Groth16 proof of the block goes through ONE GpuVerifier::verify call.
+use super::{prep_joinsplit, prep_output, prep_spend, GpuError, GpuVerifier, Item};
+use super::{ZG_KIND_OUTPUT, ZG_KIND_SPEND, ZG_KIND_SPROUT, ZG_STATUS_OK};
+
+pub struct JoinSplit {
+    pub anchor: [u8; 32],
+    pub random_seed: [u8; 32],
+    pub nullifiers: [[u8; 32]; 2],
+    pub macs: [[u8; 32]; 2],
+    pub commitments: [[u8; 32]; 2],
+    pub vpub_old: u64,
+    pub vpub_new: u64,
+    /// 192-byte Groth16 proof (v4+); None for a PGHR13 description (verdict in `pghr_ok`)
+    pub groth_proof: Option<[u8; 192]>,
+    pub pghr_ok: bool,
+    /// the caller's tree_cache.continue_root outcome (accept_transaction.rs:589)
+    pub tree_error: Option<String>,
+}
+
+pub struct Spend {
+    pub cv: [u8; 32],
+    pub anchor: [u8; 32],
+    pub nullifier: [u8; 32],
+    pub rk: [u8; 32],
+    pub zkproof: [u8; 192],
+    /// the caller's RedJubjub spend_auth_sig verdict
+    pub sig_ok: bool,
+}
+
+pub struct Output {
+    pub cv: [u8; 32],
+    pub cmu: [u8; 32],
+    pub epk: [u8; 32],
+    pub zkproof: [u8; 192],
+}
+
+#[derive(Default)]
+pub struct Tx {
+    /// first failing check before the JoinSplit stage (version ... eval)
+    pub pre_error: Option<String>,
+    pub js_pubkey: Option<[u8; 32]>,
+    pub js_sig_ok: bool,
+    pub joinsplits: Vec<JoinSplit>,
+    pub js_nullifier_error: Option<String>,
+    pub spends: Vec<Spend>,
+    pub outputs: Vec<Output>,
+    pub binding_ok: bool,
+    pub sapling_nullifier_error: Option<String>,
+}
+
+#[derive(Debug, Clone, PartialEq)]
+pub enum TxError {
+    Caller(String),
+    JoinSplitSignature,
+    InvalidJoinSplit(usize),
+    InvalidSapling,
+}
+
+enum Plan {
+    Proof(usize),
+    Caller(bool),
+    Prep,
+}
+
+fn queue(txs: &[Tx]) -> (Vec<Item>, Vec<(Vec<Plan>, Vec<Plan>, Vec<Plan>)>) {
+    let mut items = Vec::new();
+    let mut plans = Vec::new();
+    for tx in txs {
+        let (mut js, mut sp, mut out) = (Vec::new(), Vec::new(), Vec::new());
+        for d in &tx.joinsplits {
+            match (&d.groth_proof, &tx.js_pubkey) {
+                (Some(p), Some(pk)) => {
+                    let inputs = prep_joinsplit(&d.anchor, &d.random_seed, &d.nullifiers, &d.macs, &d.commitments,
+                                                d.vpub_old, d.vpub_new, pk);
+                    js.push(Plan::Proof(items.len()));
+                    items.push(Item { proof: *p, kind: ZG_KIND_SPROUT, inputs });
+                }
+                _ => js.push(Plan::Caller(d.pghr_ok)),
+            }
+        }
+        for s in &tx.spends {
+            match prep_spend(&s.cv, &s.anchor, &s.nullifier, &s.rk) {
+                Ok(inputs) => {
+                    sp.push(Plan::Proof(items.len()));
+                    items.push(Item { proof: s.zkproof, kind: ZG_KIND_SPEND, inputs });
+                }
+                Err(_) => sp.push(Plan::Prep),
+            }
+        }
+        for o in &tx.outputs {
+            match prep_output(&o.cv, &o.cmu, &o.epk) {
+                Ok(inputs) => {
+                    out.push(Plan::Proof(items.len()));
+                    items.push(Item { proof: o.zkproof, kind: ZG_KIND_OUTPUT, inputs });
+                }
+                Err(_) => out.push(Plan::Prep),
+            }
+        }
+        plans.push((js, sp, out));
+    }
+    (items, plans)
+}
+
+fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8]) -> Option<TxError> {
+    let (js, sp, out) = plan;
+    if let Some(e) = &tx.pre_error {
+        return Some(TxError::Caller(e.clone()));
+    }
+    if !tx.joinsplits.is_empty() {
+        if !tx.js_sig_ok {
+            return Some(TxError::JoinSplitSignature);
+        }
+        for (i, (d, p)) in tx.joinsplits.iter().zip(js).enumerate() {
+            let ok = match p {
+                Plan::Proof(k) => status[*k] == ZG_STATUS_OK,
+                Plan::Caller(v) => *v,
+                Plan::Prep => false,
+            };
+            if !ok {
+                return Some(TxError::InvalidJoinSplit(i));
+            }
+            if let Some(e) = &d.tree_error {
+                return Some(TxError::Caller(e.clone()));
+            }
+        }
+        if let Some(e) = &tx.js_nullifier_error {
+            return Some(TxError::Caller(e.clone()));
+        }
+    }
+    if !tx.spends.is_empty() || !tx.outputs.is_empty() {
+        for (s, p) in tx.spends.iter().zip(sp) {
+            let bad = match p {
+                Plan::Proof(k) => !s.sig_ok || status[*k] != ZG_STATUS_OK,
+                _ => true,
+            };
+            if bad {
+                return Some(TxError::InvalidSapling);
+            }
+        }
+        for p in out {
+            let bad = match p {
+                Plan::Proof(k) => status[*k] != ZG_STATUS_OK,
+                _ => true,
+            };
+            if bad {
+                return Some(TxError::InvalidSapling);
+            }
+        }
+        if !tx.binding_ok {
+            return Some(TxError::InvalidSapling);
+        }
+        if let Some(e) = &tx.sapling_nullifier_error {
+            return Some(TxError::Caller(e.clone()));
+        }
+    }
+    None
+}
+
+/// Check the shielded proofs of a block (or an import window: transactions in chain order).
+/// Ok(None) if every transaction passes, else Ok(Some((tx_index, error))) with the error the
+/// reference reports; Err only for a GPU / runtime failure (the caller then falls back to
+/// the CPU path).
+pub fn verify_block(v: &GpuVerifier, txs: &[Tx]) -> Result<Option<(usize, TxError)>, GpuError> {
+    let (items, plans) = queue(txs);
+    let status = if items.is_empty() { Vec::new() } else { v.verify(&items)? };
+    for (idx, (tx, plan)) in txs.iter().zip(&plans).enumerate() {
+        if let Some(e) = tx_error(tx, plan, &status) {
+            return Ok(Some((idx, e)));
+        }
+    }
+    Ok(None)
+}

@@ -1,0 +1,190 @@
+//! verification/src/gpu/mod.rs -- the MI355X batch Groth16 verifier behind Zebra's proof checks.
+//!
+//! A thin safe layer over the C ABI of include/zg.h (libzg.so, HIP for gfx950, built by
+//! build.rs). It replaces, for a whole block or import window, the per-description
+//! `Proof::<Bls12>::read` + `bellman::groth16::verify_proof` calls of
+//! verification/src/sapling.rs:157-167,202-212 and verification/src/sprout.rs:69-80; the
+//! queueing and re-injection in reference order is `collect` (a transcription of
+//! zebra_amd/collector.py, which tests/test_collector.py checks against the reference's real
+//! transactions).
+pub mod collect;
+pub mod ffi;
+
+use std::ffi::CStr;
+use std::os::raw::c_int;
+use std::sync::Mutex;
+
+pub use ffi::{ZG_KIND_OUTPUT, ZG_KIND_SPEND, ZG_KIND_SPROUT};
+pub use ffi::{ZG_STATUS_DECODE_INVALID, ZG_STATUS_MALFORMED_VK, ZG_STATUS_OK, ZG_STATUS_VERIFY_FAILED};
+
+/// A C-ABI error: the ZG_E_* code and zg_last_error's text.
+#[derive(Debug, Clone)]
+pub struct GpuError {
+    pub code: i32,
+    pub message: String,
+}
+
+/// One queued Groth16 check: the 192 proof bytes, the kind (= verifying key) and its public
+/// inputs as canonical little-endian Fr (`FrRepr::write_le`), 7 / 5 / 9 of them.
+#[derive(Clone)]
+pub struct Item {
+    pub proof: [u8; 192],
+    pub kind: u8,
+    pub inputs: Vec<[u8; 32]>,
+}
+
+/// One batch slot on one GPU (device buffers only; the streams and the prepared verifying keys
+/// are shared per device inside libzg). Several slots keep several windows in flight.
+pub struct GpuVerifier {
+    ctx: *mut ffi::ZgCtx,
+    max_batch: usize,
+    lock: Mutex<()>,
+}
+unsafe impl Send for GpuVerifier {}
+unsafe impl Sync for GpuVerifier {}
+
+fn last_error(ctx: *mut ffi::ZgCtx) -> String {
+    unsafe { CStr::from_ptr(ffi::zg_last_error(ctx)) }.to_string_lossy().into_owned()
+}
+
+fn check(ctx: *mut ffi::ZgCtx, rc: c_int) -> Result<(), GpuError> {
+    if rc == ffi::ZG_OK {
+        Ok(())
+    } else {
+        Err(GpuError { code: rc, message: last_error(ctx) })
+    }
+}
+
+/// the flat layouts of zg_verify_batch: n x 192 proof bytes, n kinds, n x 288 input bytes, n counts
+fn pack(items: &[Item]) -> (Vec<u8>, Vec<u8>, Vec<u8>, Vec<u8>) {
+    let n = items.len();
+    let mut proofs = Vec::with_capacity(ffi::ZG_PROOF_BYTES * n);
+    let mut kinds = Vec::with_capacity(n);
+    let mut inputs = vec![0u8; ffi::ZG_INPUT_STRIDE * n];
+    let mut counts = Vec::with_capacity(n);
+    for (i, it) in items.iter().enumerate() {
+        proofs.extend_from_slice(&it.proof);
+        kinds.push(it.kind);
+        counts.push(it.inputs.len().min(255) as u8);
+        for (j, x) in it.inputs.iter().enumerate().take(ffi::ZG_MAX_INPUTS) {
+            let o = ffi::ZG_INPUT_STRIDE * i + ffi::ZG_FR_BYTES * j;
+            inputs[o..o + ffi::ZG_FR_BYTES].copy_from_slice(x);
+        }
+    }
+    (proofs, kinds, inputs, counts)
+}
+
+impl GpuVerifier {
+    /// A slot on `device` for batches of up to `max_batch` proofs, with the three unchanged
+    /// verifying keys of res/*.json (embedded at build time) prepared on the GPU.
+    pub fn new(device: i32, max_batch: u32) -> Result<Self, GpuError> {
+        // seeded = 0: every batch draws a fresh 256-bit getrandom(2) key, expanded on the GPU
+        // by ChaCha20 into the 128-bit batch scalars
+        let cfg = ffi::ZgConfig { device, max_batch, seeded: 0, seed: 0 };
+        let ctx = unsafe { ffi::zg_create(&cfg) };
+        if ctx.is_null() {
+            return Err(GpuError { code: ffi::ZG_E_HIP, message: last_error(std::ptr::null_mut()) });
+        }
+        let v = GpuVerifier { ctx, max_batch: if max_batch == 0 { 65536 } else { max_batch as usize }, lock: Mutex::new(()) };
+        for k in [ZG_KIND_SPEND, ZG_KIND_OUTPUT, ZG_KIND_SPROUT] {
+            check(ctx, unsafe { ffi::zg_vk_load_builtin(ctx, k as c_int) })?;
+        }
+        Ok(v)
+    }
+
+    pub fn max_batch(&self) -> usize {
+        self.max_batch
+    }
+
+    /// Every item's status (ZG_STATUS_*), exact per proof: a failing batch is bisected on the
+    /// GPU. Windows larger than max_batch go as consecutive batches.
+    pub fn verify(&self, items: &[Item]) -> Result<Vec<u8>, GpuError> {
+        let _g = self.lock.lock().unwrap();
+        let mut out = Vec::with_capacity(items.len());
+        for chunk in items.chunks(self.max_batch.max(1)) {
+            let (proofs, kinds, inputs, counts) = pack(chunk);
+            let mut status = vec![0u8; chunk.len()];
+            check(self.ctx, unsafe {
+                ffi::zg_verify_batch(self.ctx, chunk.len(), proofs.as_ptr(), kinds.as_ptr(), inputs.as_ptr(),
+                                     counts.as_ptr(), std::ptr::null(), status.as_mut_ptr(), std::ptr::null_mut())
+            })?;
+            out.extend_from_slice(&status);
+        }
+        Ok(out)
+    }
+
+    /// Multi-GPU split (one process per GPU): queue this rank's shard and return its 576-byte
+    /// Miller partial. Gather the partials of all ranks (RCCL all-gather), then `verdict` and
+    /// `finish` on every rank.
+    pub fn begin_partial(&self, items: &[Item]) -> Result<[u8; 576], GpuError> {
+        let (proofs, kinds, inputs, counts) = pack(items);
+        check(self.ctx, unsafe {
+            ffi::zg_batch_begin(self.ctx, items.len(), proofs.as_ptr(), kinds.as_ptr(), inputs.as_ptr(),
+                                counts.as_ptr(), std::ptr::null())
+        })?;
+        let mut part = [0u8; 576];
+        check(self.ctx, unsafe { ffi::zg_batch_partial(self.ctx, part.as_mut_ptr()) })?;
+        Ok(part)
+    }
+
+    /// ONE final exponentiation of the product of all ranks' partials: the batch verdict.
+    pub fn verdict(&self, partials: &[[u8; 576]]) -> Result<bool, GpuError> {
+        let flat: Vec<u8> = partials.iter().flat_map(|p| p.iter().copied()).collect();
+        let mut ok: c_int = 0;
+        check(self.ctx, unsafe { ffi::zg_gt_check(self.ctx, partials.len(), flat.as_ptr(), &mut ok) })?;
+        Ok(ok != 0)
+    }
+
+    /// Per-proof statuses of this rank's shard; a false verdict bisects the shard.
+    pub fn finish(&self, n: usize, batch_ok: bool) -> Result<Vec<u8>, GpuError> {
+        let mut status = vec![0u8; n];
+        check(self.ctx, unsafe { ffi::zg_batch_finish(self.ctx, batch_ok as c_int, status.as_mut_ptr()) })?;
+        Ok(status)
+    }
+}
+
+impl Drop for GpuVerifier {
+    fn drop(&mut self) {
+        unsafe { ffi::zg_destroy(self.ctx) }
+    }
+}
+
+/// The Groth16 public-input preparation of the reference, restated in libzg (CPU only):
+/// accept_spend (sapling.rs:101-155) -> 7 Fr, or the ZG_PREP_* error class.
+pub fn prep_spend(cv: &[u8; 32], anchor: &[u8; 32], nullifier: &[u8; 32], rk: &[u8; 32]) -> Result<Vec<[u8; 32]>, i32> {
+    let mut out = [0u8; 7 * 32];
+    let rc = unsafe { ffi::zg_prep_spend(cv.as_ptr(), anchor.as_ptr(), nullifier.as_ptr(), rk.as_ptr(), out.as_mut_ptr()) };
+    if rc != 0 {
+        return Err(rc);
+    }
+    Ok(out.chunks(32).map(|c| c.try_into().unwrap()).collect())
+}
+
+/// accept_output (sapling.rs:171-200) -> 5 Fr
+pub fn prep_output(cv: &[u8; 32], cmu: &[u8; 32], epk: &[u8; 32]) -> Result<Vec<[u8; 32]>, i32> {
+    let mut out = [0u8; 5 * 32];
+    let rc = unsafe { ffi::zg_prep_output(cv.as_ptr(), cmu.as_ptr(), epk.as_ptr(), out.as_mut_ptr()) };
+    if rc != 0 {
+        return Err(rc);
+    }
+    Ok(out.chunks(32).map(|c| c.try_into().unwrap()).collect())
+}
+
+/// sprout::verify's input (sprout.rs:34-58,86-153) -> 9 Fr
+#[allow(clippy::too_many_arguments)]
+pub fn prep_joinsplit(anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[u8; 32]; 2], macs: &[[u8; 32]; 2],
+                      commitments: &[[u8; 32]; 2], vpub_old: u64, vpub_new: u64, pubkey: &[u8; 32]) -> Vec<[u8; 32]> {
+    let cat = |x: &[[u8; 32]; 2]| -> [u8; 64] {
+        let mut o = [0u8; 64];
+        o[..32].copy_from_slice(&x[0]);
+        o[32..].copy_from_slice(&x[1]);
+        o
+    };
+    let (nf, mc, cm) = (cat(nullifiers), cat(macs), cat(commitments));
+    let mut out = [0u8; 9 * 32];
+    unsafe {
+        ffi::zg_prep_joinsplit(anchor.as_ptr(), random_seed.as_ptr(), nf.as_ptr(), mc.as_ptr(), cm.as_ptr(), vpub_old,
+                               vpub_new, pubkey.as_ptr(), out.as_mut_ptr());
+    }
+    out.chunks(32).map(|c| c.try_into().unwrap()).collect()
+}

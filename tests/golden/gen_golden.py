@@ -183,9 +183,17 @@ def main():
     # ---------------------------------------------------------------- proof mutants
     mutants = []
 
+    # the reference's own tests fix the error class of these mutants: the oracle
+    # must land every one of them in that class, or the fixtures are not written
+    pinned_class = {"zero_proof": G.DECODE_INVALID, "bad_vk_empty_ic": G.MALFORMED_VK,
+                    "nullifier_zeroed": G.VERIFY_FAILED, "cmu_is_cv": G.VERIFY_FAILED}
+
     def mut(name, kind, proof, inputs, vk="builtin", n_inputs=None, pinned=None):
         pvk = pvks[kind] if vk == "builtin" else G.prepare_verifying_key(G.bad_verifying_key())
         st, gt = G.verify_status(pvk, proof, inputs, n_inputs)
+        if pinned:
+            want = pinned_class[name.split(":", 1)[1]]
+            assert st == want, "%s: oracle class %d, reference pins %d (%s)" % (name, st, want, pinned)
         mutants.append({"name": name, "kind": kind, "proof": hx(proof), "inputs": [fr_hex(v) for v in inputs],
                         "vk": vk, "status": st, "lhs_gt": hx(B.f12_to_bytes(gt)) if gt is not None else None,
                         "pinned_by": pinned})
@@ -349,6 +357,43 @@ def main():
         print("wrote", fn)
 
 
+def gen_vk_codec():
+    """crypto/src/json/groth16.rs:108-148: the reference's uncompressed-point codec vectors (a
+    valid G1 and G2, too few / too many hex chars, halves swapped -> not on the curve), copied as
+    data into vk_codec.json with the outcome each test asserts; the oracle must agree."""
+    import re
+    src = open(os.path.join(REF, "crypto/src/json/groth16.rs")).read()
+    tests = {}
+    for name in ("g1", "g1_messed", "g2", "g2_messed"):
+        m = re.search(r"fn %s\(\) \{(.*?)\n\t\}" % name, src, re.S)
+        tests[name] = re.findall(r'r#""(0x[0-9a-fA-F]*)""#', m.group(1))
+    labels = {"g1": ["valid"], "g1_messed": ["too_few_chars", "too_many_chars", "invalid_curve_point"],
+              "g2": ["valid"], "g2_messed": ["too_few_chars", "too_many_chars", "invalid_curve_point"]}
+    vecs = []
+    for name, hexes in tests.items():
+        assert len(hexes) == len(labels[name]), (name, len(hexes))
+        group = name[:2]
+        for lab, h in zip(labels[name], hexes):
+            ok = lab == "valid"
+            raw = bytes.fromhex(h[2:])
+            try:
+                want_len = 96 if group == "g1" else 192
+                if len(raw) != want_len:
+                    raise B.DecodeError("Expected hex string of length %d" % want_len)
+                (B.g1_decode_uncompressed if group == "g1" else B.g2_decode_uncompressed)(raw)
+                got = True
+            except B.DecodeError:
+                got = False
+            assert got == ok, (name, lab)
+            vecs.append({"group": group, "case": lab, "hex": h, "ok": ok,
+                         "pinned_by": "crypto/src/json/groth16.rs:%s" % ("109-112" if name == "g1" else
+                                                                        "114-127" if name == "g1_messed" else
+                                                                        "129-133" if name == "g2" else "135-148")})
+    with open(os.path.join(HERE, "vk_codec.json"), "w") as f:
+        json.dump({"vectors": vecs}, f, indent=1, sort_keys=True)
+    print("wrote vk_codec.json", len(vecs))
+
+
 def refresh_batch_gt():
     """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
     change of the batch-scalar mapping; no reference sources needed)"""
@@ -370,5 +415,7 @@ def refresh_batch_gt():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--refresh-batch-gt":
         refresh_batch_gt()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--vk-codec":
+        gen_vk_codec()
     else:
         main()

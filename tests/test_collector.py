@@ -103,6 +103,30 @@ def test_error_precedence(cpu_verify):
     assert verify_block(t, verify=cpu_verify) == (1, ("InvalidJoinSplit", 0))
 
 
+def test_window_larger_than_max_batch(cpu_verify):
+    """an import window with more proofs than one batch holds is verified as
+    consecutive batches (verify.max_batch = 3 here) with the statuses joined in order: same
+    outcome, same error position as one batch"""
+    from zebra_amd.collector import verify_block
+    F = fields()
+    calls = []
+
+    def small(proofs, kinds, inputs, n_inputs):
+        assert len(kinds) <= 3
+        calls.append(len(kinds))
+        return cpu_verify(proofs, kinds, inputs, n_inputs)
+    small.max_batch = 3
+    txs = [make_tx(v, F) for v in SRC_TX.values()]
+    assert verify_block(txs, verify=small) is None
+    assert sum(calls) == 9 and max(calls) == 3 and len(calls) == 3
+    bad = bytearray(h(F["O2"]["zkproof"]))
+    bad[150] ^= 1
+    txs[3].outputs[0].zkproof = bytes(bad)
+    calls.clear()
+    assert verify_block(txs, verify=small) == (3, "InvalidSapling")
+    assert verify_block(txs, verify=cpu_verify) == (3, "InvalidSapling")
+
+
 @pytest.mark.gpu
 def test_config5_replay_block_stream():
     """config 5: blocks of re-randomized real transactions, Sprout-Groth16 : Sapling = 1 : 4 by

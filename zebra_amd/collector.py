@@ -143,17 +143,41 @@ def _tx_error(tx, plan, status):
     return None
 
 
+def _chunked(verify, cap):
+    """an import window larger than one batch (the context's max_batch) is verified as
+    consecutive batches of at most `cap` proofs; statuses are joined in order (per-proof
+    statuses do not depend on how proofs are grouped into batches)"""
+    if not cap:
+        return verify
+
+    def run(proofs, kinds, inputs, n_inputs):
+        n = len(kinds)
+        out = []
+        for lo in range(0, n, cap):
+            hi = min(n, lo + cap)
+            out += list(verify(proofs[192 * lo:192 * hi], kinds[lo:hi], inputs[zg.INPUT_STRIDE * lo:zg.INPUT_STRIDE * hi],
+                               n_inputs[lo:hi]))
+        return out
+    return run
+
+
 def verify_block(txs, verify=None, ctx=None):
     """Check the shielded proofs of a block (or an import window: a flat list of Tx in chain
     order). Returns None if every transaction passes, else (tx_index, error) with the error the
     reference reports (accept_chain.rs:79-80: the lowest failing index wins).
 
     verify(proofs, kinds, inputs, n_inputs) -> statuses; default: ctx.verify_batch (ONE GPU
-    batch for the whole block, exact per-proof statuses via bisection)."""
+    batch for the whole block, exact per-proof statuses via bisection). A window larger than
+    the context's max_batch (or a `verify.max_batch` attribute) is split into consecutive
+    batches."""
     items, plans = _queue(txs)
     if verify is None:
         def verify(proofs, kinds, inputs, n_inputs):
             return ctx.verify_batch(proofs, kinds, inputs, n_inputs)[0]
+        cap = getattr(ctx, "max_batch", None)
+    else:
+        cap = getattr(verify, "max_batch", None)
+    verify = _chunked(verify, cap)
     status = []
     if items:
         proofs = b"".join(p for _, p, _ in items)

@@ -25,9 +25,9 @@ using namespace zg;
 
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
-#define ZG_NEV 8
-#define ZG_NTIMINGS 7
-#define ZG_NSTATS 6
+#define ZG_NEV 13
+#define ZG_NTIMINGS 9
+#define ZG_NSTATS 7
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
 
@@ -84,6 +84,8 @@ struct zg_ctx {
   int ncu = 0;            // compute units of the device
   int fuse = -1;          // ZG_LINES_FCHAIN: -1 auto (both grids resident at once), 0 never, 1 always
   int fuse_off = 0;       // a fused launch ever timed out waiting: split launches from then on
+  int serial_side = 0;    // ZG_SERIAL_SIDE=1: the side-stream work runs on the main stream after the
+                          // product tree (measurement: the Miller kernels alone on the device)
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
@@ -91,6 +93,7 @@ struct zg_ctx {
   Fr* d_stree = nullptr;
   MsmBufs msm = {};       // K4: Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)
   int trees_built = 0;    // the full C / Fr trees exist for this batch (bisection only)
+  int c_tree_pending = 0; // the C tree is still being built on the side stream (ev[12])
   // node checks
   int* d_nodes = nullptr;
   G1J* d_msm = nullptr;
@@ -106,7 +109,8 @@ struct zg_ctx {
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
   // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
-  // (bfail, deferred recomputes), [4] bisections, [5] nodes checked by bisection
+  // (bfail, deferred recomputes), [4] bisections, [5] nodes checked by bisection,
+  // [6] K4 bucket entries of the last batch (points with a non-zero digit, summed over windows)
   uint64_t stats[ZG_NSTATS] = {};
   uint64_t calls = 0;
 };
@@ -209,6 +213,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ctx->stream = dev->main[ctx->pair];
   ctx->side = dev->side[ctx->pair];
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
+  if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
     if (e == hipSuccess) e = r;
@@ -574,7 +579,8 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 
 namespace zg {
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);          // zg_decode.hip
-hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate);  // zg_msm.hip
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate,
+                           hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr);          // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
 }
 
@@ -595,15 +601,24 @@ static int run_pipeline(zg_ctx* ctx) {
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
   HIPCHK(launch_batch_decode(dgroups, ctx->stream, b));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-  // side stream
-  HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
-  HIPCHK(hipEventRecord(ctx->ev[5], ctx->side));
   ctx->trees_built = 0;
-  HIPCHK(launch_msm_root(ctx->side, b, ctx->msm, nullptr));
+  ctx->c_tree_pending = 0;
   NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
-  int rc = launch_node_msm_pairs(ctx, b, nb, ctx->side);
-  if (rc) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[6], ctx->side));
+  // side stream: K4 + the root's VK-side work (or, serial_side, on the main stream after the tree)
+  auto side_work = [&](hipStream_t st) -> int {
+    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9]));
+    HIPCHK(hipEventRecord(ctx->ev[10], st));
+    int r = launch_node_msm_pairs(ctx, b, nb, st);
+    if (r) return r;
+    HIPCHK(hipEventRecord(ctx->ev[6], st));
+    return ZG_OK;
+  };
+  int rc;
+  if (!ctx->serial_side) {
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
+    if ((rc = side_work(ctx->side))) return rc;
+  }
   // main stream: the R-chain (lines; also the G2 subgroup checks of the B_i), then the f-chain
   // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
@@ -635,12 +650,16 @@ static int run_pipeline(zg_ctx* ctx) {
       hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream trees + root pairs complete
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  if (ctx->serial_side) {
+    if ((rc = side_work(ctx->stream))) return rc;
+  } else {
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream K4 + root pairs complete
+  }
   // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
   HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail));
   rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
   if (rc) return rc;
-  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   ctx->root_pairs_ready = 1;
   return ZG_OK;
 }
@@ -725,7 +744,10 @@ extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs
   return ZG_OK;
 }
 
-// check a list of tree nodes; mode per k_node_final. ok / out are host arrays (may be null)
+// check a list of tree nodes; mode per k_node_final. ok / out are host arrays (may be null).
+// The per-proof Miller leaves (leaf f-chain from the stored line triples) run on the side stream
+// while the main stream runs the nodes' VK-side MSM and Miller loops; the final exponentiations
+// wait for both.
 static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std::vector<int>* ok, uint8_t* out_bytes) {
   BatchBufs b = batch_bufs(ctx);
   if (ok) ok->assign(nodes.size(), 0);
@@ -737,16 +759,27 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
     if (!reuse_root) {
       ctx->root_pairs_ready = 0;  // d_msm / d_pairf are about to be overwritten
       HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
-      int rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream);
-      if (rc) return rc;
-      // per-proof Miller leaves exist only on demand (the f-chain writes pair nodes)
       bool leaves = false;
       for (int q = 0; q < m; q++) leaves = leaves || nodes[off + q] >= (int)ctx->npad;
-      if (leaves) {
-        hipLaunchKernelGGL(k_leaf_miller, dim3(nblocks(m)), dim3(ZG_BLOCK), 0, ctx->stream, b, (const int*)ctx->d_nodes,
-                           m);
+      if (leaves) {  // per-proof Miller leaves exist only on demand (the f-chain writes pair nodes)
+        HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
+        HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
+        hipLaunchKernelGGL(k_leaf_fchain, dim3(nblocks(m)), dim3(64 * ZG_FC_NW), 0, ctx->side, b,
+                           (const Fq2*)ctx->d_lines, (const int*)ctx->d_nodes, m);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev[11], ctx->side));
       }
+      hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS)),
+                         dim3(ZG_BLOCK), 0, ctx->stream, b, nb, (const int*)nullptr);
+      HIPCHK(hipGetLastError());
+      if (ctx->c_tree_pending) {  // the C tree (side stream) feeds the delta pairs
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[12], 0));
+        ctx->c_tree_pending = 0;
+      }
+      hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, ctx->stream, b, nb,
+                         (const int*)nullptr);
+      HIPCHK(hipGetLastError());
+      if (leaves) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[11], 0));
     }
     hipLaunchKernelGGL(k_node_final, dim3(m), dim3(64), 0, ctx->stream, b, nb, mode);
     HIPCHK(hipGetLastError());
@@ -764,8 +797,9 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
 // forced the gated recompute; a fused launch whose consumers timed out waiting, which turns
 // the fused shape off for this context)
 static int collect_batch_stats(zg_ctx* ctx) {
-  int flags[2] = {0, 0};
+  int flags[2] = {0, 0}, entries = 0;
   HIPCHK(hipMemcpyAsync(flags, ctx->d_int + 8, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(&entries, ctx->msm.start + ZG_MSM_NCOUNT, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   ctx->stats[0]++;
@@ -775,13 +809,17 @@ static int collect_batch_stats(zg_ctx* ctx) {
     ctx->fuse_off = 1;
   }
   if (flags[0]) ctx->stats[3]++;
+  ctx->stats[6] = (uint64_t)entries;
   hipEventElapsedTime(&ctx->timings[0], ctx->ev[0], ctx->ev[1]);  // decode
   hipEventElapsedTime(&ctx->timings[1], ctx->ev[1], ctx->ev[7]);  // lines (R-chain)
   hipEventElapsedTime(&ctx->timings[2], ctx->ev[7], ctx->ev[2]);  // f-chain
   hipEventElapsedTime(&ctx->timings[3], ctx->ev[2], ctx->ev[3]);  // Fq12 product tree
-  hipEventElapsedTime(&ctx->timings[4], ctx->ev[3], ctx->ev[4]);  // root partial (after the side stream)
+  hipEventElapsedTime(&ctx->timings[4], ctx->ev[3], ctx->ev[4]);  // root partial: waits for the side stream
+                                                                  // (serial_side: runs it), gated recompute
   hipEventElapsedTime(&ctx->timings[5], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
   hipEventElapsedTime(&ctx->timings[6], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
+  hipEventElapsedTime(&ctx->timings[7], ctx->ev[5], ctx->ev[10]);  // K4 (Pippenger + root Fr sums)
+  hipEventElapsedTime(&ctx->timings[8], ctx->ev[8], ctx->ev[9]);   // K4 bucket phase (k_msm_bucket)
   return ZG_OK;
 }
 
@@ -842,60 +880,82 @@ extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
 // Bisection over the product trees: a failing node's children are re-checked exactly;
 // a failing leaf is a proof whose own check fails (r_i != 0 makes it bellman's check).
 // bisection needs every node's C and Fr sums: the per-proof r_i C_i (GLV) leaves and the full
-// trees, built only now (a valid batch never needs them: K4 forms the root directly)
+// trees, built only now (a valid batch never needs them: K4 forms the root directly). The Fr
+// tree (cheap; all the node MSM needs) is built on the main stream, the C leaves and tree on
+// the side stream, joined before the first delta pairs (ev[12]).
 static int build_trees(zg_ctx* ctx) {
   if (ctx->trees_built) return ZG_OK;
   BatchBufs b = batch_bufs(ctx);
-  HIPCHK(launch_c_leaves(ctx->stream, b));
+  HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
+  HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
+  HIPCHK(launch_c_leaves(ctx->side, b));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_cs, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo, (const int*)nullptr);
+    hipLaunchKernelGGL(k_tree_c, dim3(nblocks(lo * ZG_NKINDS)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_tree_s, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }
+  HIPCHK(hipEventRecord(ctx->ev[12], ctx->side));
+  ctx->c_tree_pending = 1;
   ctx->trees_built = 1;
   return ZG_OK;
 }
 
-static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st) {
-  std::vector<int> level = {1};
+// Each round checks, in one launch group, the descendants of every failing node k levels down,
+// k as large as keeps the round within ZG_BISECT_BUDGET nodes (at least one level): a round
+// costs about the same for 16 or 512 nodes (single-wave Miller loops and final
+// exponentiations, latency-bound), so few failing nodes descend many levels at once. E.g.
+// 4,096 proofs with 27 failing: 512 nodes of 8, then 216 leaves.
+#define ZG_BISECT_BUDGET 512
+static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st, bool root_failed) {
   const int npad = (int)ctx->npad, n = (int)ctx->n;
+  int depth_leaf = 0;
+  while ((1 << depth_leaf) < npad) depth_leaf++;
   ctx->stats[4]++;
   int rc0 = build_trees(ctx);
   if (rc0) return rc0;
-  while (!level.empty()) {
+  std::vector<int> fails;  // failing nodes of the last round, all at the same depth
+  if (root_failed) {
+    fails.push_back(1);
+  } else {
+    std::vector<int> ok;
+    ctx->stats[5] += 1;
+    int rc = check_nodes(ctx, std::vector<int>{1}, 0, &ok, nullptr);
+    if (rc) return rc;
+    if (!ok[0]) fails.push_back(1);
+  }
+  int d = 0;  // depth of the failing nodes
+  while (!fails.empty() && d < depth_leaf) {
+    int k = 1;
+    while (k < depth_leaf - d && fails.size() * (size_t)(2 << k) <= ZG_BISECT_BUDGET) k++;
+    std::vector<int> level;
+    for (int node : fails)  // descendants that start at or beyond n hold only padding: skipped
+      for (int c = node << k; c < (node + 1) << k; c++)
+        if (((long long)c << (depth_leaf - d - k)) - npad < n) level.push_back(c);
     std::vector<int> ok;
     ctx->stats[5] += level.size();
     int rc = check_nodes(ctx, level, 0, &ok, nullptr);
     if (rc) return rc;
-    std::vector<int> next;
-    for (size_t q = 0; q < level.size(); q++) {
-      if (ok[q]) continue;
-      int node = level[q];
-      if (node >= npad) {
-        int i = node - npad;
-        if (i < n && st[i] == ST_PENDING) st[i] = ST_VERIFY_FAILED;
-        continue;
-      }
-      // children that start at or beyond n hold only padding (identity): skip them
-      for (int c = 2 * node; c <= 2 * node + 1; c++) {
-        int x = c;
-        while (x < npad) x <<= 1;
-        int first = x - npad;
-        if (first < n) next.push_back(c);
-      }
-    }
-    level.swap(next);
+    fails.clear();
+    for (size_t q = 0; q < level.size(); q++)
+      if (!ok[q]) fails.push_back(level[q]);
+    d += k;
+  }
+  for (int node : fails) {  // failing leaves: proofs whose own check fails
+    const int i = node - npad;
+    if (i >= 0 && i < n && st[i] == ST_PENDING) st[i] = ST_VERIFY_FAILED;
   }
   return ZG_OK;
 }
 
-static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status) {
+static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool root_failed = false) {
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_finish before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
   std::vector<uint8_t> st(ctx->n);
   if (ctx->n) HIPCHK(hipMemcpyAsync(st.data(), ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (!batch_ok) {
-    int rc = bisect(ctx, st);
+    int rc = bisect(ctx, st, root_failed);
     if (rc) {
       ctx->state = 0;  // the batch is abandoned; the context stays usable
       return rc;
@@ -927,13 +987,15 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
     ctx->state = 0;
     return rc;
   }
-  return batch_finish_locked(ctx, okv[0], status);
+  return batch_finish_locked(ctx, okv[0], status, /*root_failed=*/okv[0] == 0);
 }
 
-extern "C" int zg_last_timings(zg_ctx* ctx, float* ms7) {
-  if (!ctx || !ms7) return ZG_E_INVAL;
+extern "C" int zg_last_timings(zg_ctx* ctx, float* ms7) { return zg_last_phase_ms(ctx, ms7, 7); }
+
+extern "C" int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n) {
+  if (!ctx || (n && !ms)) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
-  for (int i = 0; i < ZG_NTIMINGS; i++) ms7[i] = ctx->timings[i];
+  for (size_t i = 0; i < n; i++) ms[i] = i < ZG_NTIMINGS ? ctx->timings[i] : 0.0f;
   return ZG_OK;
 }
 

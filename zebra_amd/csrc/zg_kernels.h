@@ -221,7 +221,55 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_lines_fchain(BatchBufs b, Fq2
 }
 
 // Per-proof Miller leaves ftree[npad + i] for the listed leaf nodes (bisection below a failing
-// pair node; other nodes are skipped): pairing's miller_loop of (r_i A_i, B_i), 1 if inactive.
+// pair node; other nodes are skipped), from the line triples the R-chain left in HBM: the
+// single-proof f-chain (staged programs MSQ / M: f = (f l)^2 per step, lane = proof), 1 if the
+// proof is not active. Lanes whose node is not a leaf run on identity lines and store nothing.
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, const Fq2* lines, const int* nodes, int m) {
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  const AtomSpace at{lds_atoms};
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int q = blockIdx.x * 64 + lane;
+  const int node = q < m ? nodes[q] : -1;
+  const bool leaf = node >= b.npad && node < 2 * b.npad;
+  const int proof = leaf ? node - b.npad : 0;
+  const bool act = leaf && proof_active(b, proof);
+  auto load_lines = [&](int n) {
+    const Fq2* src = lines + ((size_t)n * b.npad + proof) * 3;
+    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? src[j] : (j == 0 ? f2_one() : f2_zero()));
+  };
+  if (wave < 6)
+    at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  else
+    load_lines(0);
+  __syncthreads();
+  int n = 0;
+  for (int i = ZG_XH_TOP;; i--) {
+    const bool last = i < 0;
+    const bool addbit = !last && ((ZG_XH >> i) & 1ull);
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
+      prog_run(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      __syncthreads();
+      n++;
+      if (wave < 6)
+        at.put(wave, v);
+      else if (n < ZG_NCOEFF)
+        load_lines(n);
+      __syncthreads();
+    }
+    if (last) break;
+  }
+  if (wave < 6 && leaf) {
+    Fq2 v = at.get(wave);
+    if (wave >= 3) v = f2_neg(v);  // conjugate (u < 0)
+    reinterpret_cast<Fq2*>(&b.ftree[node])[wave] = v;
+  }
+}
+
+// (single-lane form of the same, kept for reference and tests: pairing's miller_loop of
+// (r_i A_i, B_i) from the affine points)
 __global__ void __launch_bounds__(64) k_leaf_miller(BatchBufs b, const int* nodes, int m) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= m) return;
@@ -253,20 +301,23 @@ __global__ void __launch_bounds__(64) k_tree_f_coop(BatchBufs b, int lo) {
   coop_store(&ws, 0, b.ftree[node]);
 }
 
-// C-sum and Fr scalar-sum tree level (depends on k_batch_decode only, so it runs on the
-// side stream concurrently with the Miller kernel)
-// gate: null = always; else run only if *gate != 0 (the recompute after a deferred B failure)
-__global__ void __launch_bounds__(64) k_tree_cs(BatchBufs b, int lo, const int* gate) {
-  if (gate && *gate == 0) return;
+// C-sum and Fr scalar-sum tree levels (bisection only: a valid batch's root sums come from K4):
+// the Fr level is cheap and all the node MSM needs; the C level (Jacobian additions) only feeds
+// the delta pairs, so it is built on the side stream concurrently with the node MSM.
+__global__ void __launch_bounds__(64) k_tree_s(BatchBufs b, int lo) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= lo) return;
   const int node = lo + j, l = 2 * node, r = 2 * node + 1;
-  for (int k = 0; k < ZG_NKINDS; k++) {
-    b.ctree[node * ZG_NKINDS + k] = jac_add(b.ctree[l * ZG_NKINDS + k], b.ctree[r * ZG_NKINDS + k]);
+  for (int k = 0; k < ZG_NKINDS; k++)
     for (int m = 0; m < ZG_MAX_IC; m++)
       b.stree[(node * ZG_NKINDS + k) * ZG_MAX_IC + m] =
           fr_add(b.stree[(l * ZG_NKINDS + k) * ZG_MAX_IC + m], b.stree[(r * ZG_NKINDS + k) * ZG_MAX_IC + m]);
-  }
+}
+__global__ void __launch_bounds__(64) k_tree_c(BatchBufs b, int lo) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= lo * ZG_NKINDS) return;
+  const int node = lo + j / ZG_NKINDS, k = j % ZG_NKINDS;
+  b.ctree[node * ZG_NKINDS + k] = jac_add_full(b.ctree[2 * node * ZG_NKINDS + k], b.ctree[(2 * node + 1) * ZG_NKINDS + k]);
 }
 
 struct NodeBufs {

@@ -217,14 +217,17 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
 
 // the batch root's C sums (ctree node 1) and Fr sums (stree node 1) from the decoded batch;
 // gate: null = always, else only if *gate != 0 (the recompute after a deferred B failure)
-hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate) {
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate, hipEvent_t bucket0,
+                           hipEvent_t bucket1) {
   const unsigned pts = (unsigned)((2 * (size_t)b.npad + 63) / 64);
   hipError_t e = hipMemsetAsync(m.count, 0, sizeof(int) * ZG_MSM_NCOUNT, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_count, dim3(pts), dim3(64), 0, st, b, m, gate);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(ZG_MSM_SCAN_T), 0, st, m, gate);
   hipLaunchKernelGGL(k_msm_scatter, dim3(pts), dim3(64), 0, st, b, m, gate);
+  if (bucket0 && (e = hipEventRecord(bucket0, st)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_bucket, dim3((ZG_MSM_NCOUNT * ZG_MSM_PARTS + 63) / 64), dim3(64), 0, st, b, m, gate);
+  if (bucket1 && (e = hipEventRecord(bucket1, st)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_window, dim3(ZG_MSM_GROUPS), dim3(ZG_MSM_WT), 0, st, m, gate);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, b, m, gate);
   const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;

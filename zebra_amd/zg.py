@@ -57,6 +57,7 @@ def lib():
         L.zg_batch_finish.argtypes = [vp, i, u8p]
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
         L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+        L.zg_last_phase_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_float), sz]
         L.zg_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz]
         L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.zg_bench_mad_rate_clock.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
@@ -135,6 +136,7 @@ class Context:
 
     def __init__(self, device=0, max_batch=65536, seed=None, load_builtin=True):
         L = lib()
+        self.max_batch = max_batch
         cfg = _Config(device, max_batch, 1 if seed is not None else 0, seed or 0)
         self._p = L.zg_create(ctypes.byref(cfg))
         if not self._p:
@@ -233,14 +235,18 @@ class Context:
         self._chk(lib().zg_batch_finish(self._p, 1 if batch_ok else 0, st))
         return list(st.raw[:n])
 
+    PHASES = ("decode", "k_batch_lines", "k_batch_fchain", "k_tree_f", "root_partial", "side_stream_vk",
+              "device_pipeline", "k4_msm", "k4_bucket_phase")
+
     def last_timings(self):
-        """[decode, lines, fchain, tree, root_partial, side_stream, device_pipeline] in ms"""
-        a = (ctypes.c_float * 7)()
-        self._chk(lib().zg_last_timings(self._p, a))
+        """[decode, lines, fchain, tree, root_partial, side_stream, device_pipeline, K4, K4 bucket
+        phase] in ms (include/zg.h zg_last_phase_ms)"""
+        a = (ctypes.c_float * len(self.PHASES))()
+        self._chk(lib().zg_last_phase_ms(self._p, a, len(self.PHASES)))
         return list(a)
 
     STAT_NAMES = ("batches", "fused_launches", "fused_wait_failures", "b_subgroup_recomputes", "bisections",
-                  "bisect_nodes")
+                  "bisect_nodes", "k4_entries")
 
     def stats(self):
         """cumulative counters (include/zg.h zg_stats) as a dict"""
