@@ -188,7 +188,8 @@ def batch_gt(lhs_list, r_list):
 def batch_partial(pvks, items):
     """The Miller partial F of a shard, exactly as the GPU forms it (not final-exponentiated):
     prod_i ML(r_i A_i, B_i) * prod_k ML(acc_k, -gamma_k) ML(Csum_k, -delta_k) ML(-S_k alpha_k, beta_k)
-    over proofs that decode with a well-formed VK. items: (kind, proof bytes, inputs, r)."""
+    over proofs that decode with a well-formed VK -- with the gamma and beta pairs merged across
+    keys that share alpha, beta, gamma. items: (kind, proof bytes, inputs, r)."""
     f = B.F12_ONE
     sums = {k: [0] * len(p.ic) for k, p in pvks.items()}
     csum = {k: None for k in pvks}
@@ -208,11 +209,31 @@ def batch_partial(pvks, items):
         for j, x in enumerate(inputs):
             sums[kind][j + 1] = (sums[kind][j + 1] + r * x) % B.R
         csum[kind] = B.ec_add(B.FQ, csum[kind], B.ec_mul(B.FQ, c, r))
+    # keys sharing alpha, beta and gamma (the three Zcash keys): FE is bilinear, so the GPU merges
+    # their gamma pairs into ONE (sum_k acc_k, -gamma) and their beta pairs into ONE
+    # (-(sum_k S_k0) alpha, beta) next to one delta pair per key (zebra_amd/csrc/zg_batch.h)
+    ks = list(pvks)
+    merged = all(pvks[k].vk.alpha_g1 == pvks[ks[0]].vk.alpha_g1 and pvks[k].vk.beta_g2 == pvks[ks[0]].vk.beta_g2
+                 and pvks[k].vk.gamma_g2 == pvks[ks[0]].vk.gamma_g2 for k in ks)
+    accs = {}
     for kind, pvk in pvks.items():
         acc = None
         for s, base in zip(sums[kind], pvk.ic):
             acc = B.ec_add(B.FQ, acc, B.ec_mul(B.FQ, base, s))
+        accs[kind] = acc
+    if merged:
+        p0 = pvks[ks[0]]
+        gsum = None
+        for k in ks:
+            gsum = B.ec_add(B.FQ, gsum, accs[k])
+        nsa = B.ec_mul(B.FQ, p0.vk.alpha_g1, (-sum(sums[k][0] for k in ks)) % B.R)
+        pairs = [(gsum, p0.neg_gamma_g2)] + [(csum[k], pvks[k].neg_delta_g2) for k in ks] + \
+            [(nsa, B.g2_prepare(p0.vk.beta_g2))]
+        for pr in pairs:   # each pair's Miller loop on its own, multiplied (as the GPU does)
+            f = B.f12_mul(f, B.miller_loop([pr]))
+        return f
+    for kind, pvk in pvks.items():
         nsa = B.ec_mul(B.FQ, pvk.vk.alpha_g1, (-sums[kind][0]) % B.R)
-        f = B.f12_mul(f, B.miller_loop([(acc, pvk.neg_gamma_g2), (csum[kind], pvk.neg_delta_g2),
+        f = B.f12_mul(f, B.miller_loop([(accs[kind], pvk.neg_gamma_g2), (csum[kind], pvk.neg_delta_g2),
                                          (nsa, B.g2_prepare(pvk.vk.beta_g2))]))
     return f

@@ -103,7 +103,7 @@ int zgt_vk_prepare(const uint8_t* raw_fields /*96+96+192+192+96+192*/, int n_ic,
   memcpy(raw.delta_g2, p, 192);
   raw.n_ic = n_ic;
   for (int i = 0; i < n_ic; i++) memcpy(raw.ic[i], ic + 96 * i, 96);
-  int r = vk_prepare(raw, &g_vk);
+  int r = vk_prepare(raw, &g_vk, nullptr);
   if (r == 0) f12_to_bytes(g_vk.alpha_beta, ab);
   return r;
 }

@@ -51,6 +51,7 @@ struct zg_dev {
   struct VKEntry {
     RawVK raw;
     DevVK* d = nullptr;
+    uint32_t* comb = nullptr;  // the key's comb tables (ZG_COMB_POINTS x 96 B, k_vk_comb)
     int err = 0;
   };
   std::vector<VKEntry*> vks;  // prepare_verifying_key once per distinct key per device
@@ -73,6 +74,8 @@ struct zg_ctx {
   uint64_t seed = 0;
   int vk_loaded[ZG_NKINDS] = {0, 0, 0};
   int vk_iclen[ZG_NKINDS] = {0, 0, 0};
+  RawVK vk_raw[ZG_NKINDS];  // host copies of the loaded keys (shared alpha / beta / gamma test)
+  int merged = 0;           // loaded keys share alpha, beta, gamma: merged VK-side pairs (zg_batch.h)
   DevVK* d_vk = nullptr;  // this slot's 3 kinds (copied from the device cache)
   int* d_int = nullptr;   // scratch ints: [8] bfail, [9] fused-wait failure
   // batch
@@ -148,6 +151,7 @@ static void dev_release(zg_dev* d) {
   if (d->hi_side) hipStreamDestroy(d->hi_side);
   for (auto* e : d->vks) {
     if (e->d) hipFree(e->d);
+    if (e->comb) hipFree(e->comb);
     delete e;
   }
   g_devs[d->device] = nullptr;
@@ -245,7 +249,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->msm.frpart, ((size_t)cap / ZG_FR_CHUNK + 1) * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->d_nodes, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS));
-  A(dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_NPAIRS));
+  A(dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NODE_PAIRS));
   A(dalloc(&ctx->d_ok, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_out, ZG_NODE_CHUNK));
   for (int i = 0; i < ZG_NEV; i++) A(hipEventCreate(&ctx->ev[i]));
@@ -285,6 +289,23 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
 }
 
 // ------------------------------------------------------------------ verifying keys
+// the loaded keys share alpha_g1, beta_g2 and gamma_g2 (byte-identical): their gamma pairs and
+// their beta pairs merge (zg_batch.h ZG_NODE_PAIRS_MERGED)
+static void update_merged(zg_ctx* ctx) {
+  int first = -1, same = 1;
+  for (int k = 0; k < ZG_NKINDS; k++) {
+    if (!ctx->vk_loaded[k]) continue;
+    if (first < 0) {
+      first = k;
+      continue;
+    }
+    const RawVK &a = ctx->vk_raw[first], &c = ctx->vk_raw[k];
+    same = same && !memcmp(a.alpha_g1, c.alpha_g1, 96) && !memcmp(a.beta_g2, c.beta_g2, 192) &&
+           !memcmp(a.gamma_g2, c.gamma_g2, 192);
+  }
+  ctx->merged = same;
+}
+
 // prepare_verifying_key runs once per distinct key per device (k_vk_prepare, one thread,
 // ~140 ms); every further slot that loads the same key gets a device-to-device copy.
 static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
@@ -303,11 +324,18 @@ static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
       ent->raw = raw;
       RawVK* d_raw = nullptr;
       hipError_t e = hipMalloc(&ent->d, sizeof(DevVK));
+      if (e == hipSuccess) e = hipMalloc(&ent->comb, sizeof(uint32_t) * ZG_COMB_WORDS * (size_t)ZG_COMB_POINTS);
       if (e == hipSuccess) e = hipMalloc(&d_raw, sizeof(RawVK));
       if (e == hipSuccess) e = hipMemcpyAsync(d_raw, &raw, sizeof(RawVK), hipMemcpyHostToDevice, ctx->stream);
       if (e == hipSuccess) e = hipMemsetAsync(ent->d, 0, sizeof(DevVK), ctx->stream);
       if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_vk_prepare, dim3(1), dim3(1), 0, ctx->stream, d_raw, ent->d, ctx->d_int);
+        hipLaunchKernelGGL(k_vk_prepare, dim3(1), dim3(1), 0, ctx->stream, d_raw, ent->d, ctx->d_int,
+                           (const uint32_t*)ent->comb);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_vk_comb, dim3((ZG_COMB_POINTS + 63) / 64), dim3(64), 0, ctx->stream,
+                           (const DevVK*)ent->d, ent->comb);
         e = hipGetLastError();
       }
       if (e == hipSuccess) e = hipMemcpyAsync(&ent->err, ctx->d_int, sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
@@ -315,6 +343,7 @@ static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
       if (d_raw) hipFree(d_raw);
       if (e != hipSuccess) {
         if (ent->d) hipFree(ent->d);
+        if (ent->comb) hipFree(ent->comb);
         delete ent;
         return fail(ctx, ZG_E_HIP, std::string("prepare_verifying_key: ") + hipGetErrorString(e));
       }
@@ -325,12 +354,15 @@ static int vk_upload(zg_ctx* ctx, int kind, const RawVK& raw) {
     HIPCHK(hipMemsetAsync(ctx->d_vk + kind, 0, sizeof(DevVK), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->vk_loaded[kind] = 0;
+    update_merged(ctx);
     return fail(ctx, ZG_E_VK, "Invalid curve point in verifying key (field " + std::to_string(ent->err) + ")");
   }
   HIPCHK(hipMemcpyAsync(ctx->d_vk + kind, ent->d, sizeof(DevVK), hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->vk_loaded[kind] = 1;
   ctx->vk_iclen[kind] = raw.n_ic;
+  ctx->vk_raw[kind] = raw;
+  update_merged(ctx);
   return ZG_OK;
 }
 
@@ -562,6 +594,7 @@ static BatchBufs batch_bufs(zg_ctx* ctx) {
   b.stree = ctx->d_stree;
   b.bfail = ctx->d_int + 8;
   b.okbits = ctx->d_okbits;
+  b.merged = ctx->merged;
   b.n = (int)ctx->n;
   b.npad = (int)ctx->npad;
   return b;
@@ -572,7 +605,8 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
   hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS)), dim3(ZG_BLOCK),
                      0, st, b, nb, gate);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, st, b, nb, gate);
+  hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * (b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS)), dim3(64), 0, st,
+                     b, nb, gate);
   HIPCHK(hipGetLastError());
   return ZG_OK;
 }
@@ -776,7 +810,8 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[12], 0));
         ctx->c_tree_pending = 0;
       }
-      hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * ZG_NKINDS * ZG_NPAIRS), dim3(64), 0, ctx->stream, b, nb,
+      hipLaunchKernelGGL(k_node_pairs, dim3(nb.m * (b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS)), dim3(64), 0,
+                         ctx->stream, b, nb,
                          (const int*)nullptr);
       HIPCHK(hipGetLastError());
       if (leaves) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[11], 0));

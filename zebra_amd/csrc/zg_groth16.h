@@ -23,16 +23,18 @@ enum : uint8_t {
 #define ZG_MAX_IC 10
 #define ZG_MAX_INPUTS 9
 #define ZG_NKINDS 3
-#define ZG_SHIFTS 8  // 255-bit scalars as 8 x 32-bit chunks
+#define ZG_SHIFTS 8  // lanes per VK-side scalar (4 byte-digits of the comb each)
 
-// [2^(32 w)] p for w = 0..7 (affine)
-ZG_NOINL inline void g1_shift_table(const G1A& p, G1A* out) {
-  G1J cur = jac_from_aff(p);
-  for (int w = 0; w < ZG_SHIFTS; w++) {
-    out[w] = jac_to_aff(cur);
-    for (int d = 0; d < 32; d++) cur = jac_dbl(cur);
-  }
-}
+// Fixed-base comb tables of the VK-side MSM (k_node_msm): for each base B (ic[0..9], alpha)
+// the affine multiples d * 2^(8 w) * B, w = 0..31, d = 1..255, so a 255-bit scalar is the sum of
+// its 32 byte-digits' table points -- 32 mixed additions split over ZG_SHIFTS = 8 lanes
+// (4 each), no doublings. 33 bases x 8,160 points x 96 B = 25.8 MB per device: HBM is plentiful,
+// the latency of every VK-side MSM (batch roots and bisection nodes) is what counts.
+#define ZG_COMB_BASES (ZG_MAX_IC + 1)
+#define ZG_COMB_W 32
+#define ZG_COMB_D 255
+#define ZG_COMB_WORDS 24  // x, y Montgomery limbs
+#define ZG_COMB_POINTS (ZG_COMB_BASES * ZG_COMB_W * ZG_COMB_D)
 
 // A prepared verifying key, resident in HBM.
 struct DevVK {
@@ -45,10 +47,9 @@ struct DevVK {
   Line neg_gamma_lines[ZG_NCOEFF]; // G2Prepared(-gamma)
   Line neg_delta_lines[ZG_NCOEFF]; // G2Prepared(-delta)
   Line beta_lines[ZG_NCOEFF];      // G2Prepared(beta)  (batch alpha/beta term)
-  // fixed-base tables for the batch's VK-side MSM: [2^(32 w)] ic[j] and [2^(32 w)] alpha,
-  // so a 255-bit scalar multiplication splits into 8 independent 32-bit ones
-  G1A ic_sh[ZG_MAX_IC][ZG_SHIFTS];
-  G1A alpha_sh[ZG_SHIFTS];
+  // comb tables of ic[0..9] and alpha (base 10), ZG_COMB_W x ZG_COMB_D points each, in a
+  // per-device buffer shared by every context that loaded this key (k_vk_comb fills it)
+  const uint32_t* comb;
 };
 
 // Raw uncompressed VK as uploaded by the host (crypto/src/json/groth16.rs:33-49 fields).
@@ -59,7 +60,8 @@ struct RawVK {
 };
 
 // prepare_verifying_key. Returns 0 on success, 1 + field index on a decode failure.
-ZG_NOINL inline int vk_prepare(const RawVK& raw, DevVK* vk) {
+ZG_NOINL inline int vk_prepare(const RawVK& raw, DevVK* vk, const uint32_t* comb) {
+  vk->comb = comb;
   G1A beta_g1, delta_g1;
   if (g1_decode_uncompressed(raw.alpha_g1, &vk->alpha) == DEC_ERR) return 1;
   if (g1_decode_uncompressed(raw.beta_g1, &beta_g1) == DEC_ERR) return 2;
@@ -81,8 +83,6 @@ ZG_NOINL inline int vk_prepare(const RawVK& raw, DevVK* vk) {
   if (!ng.inf) g2_prepare(ng, vk->neg_gamma_lines);
   if (!nd.inf) g2_prepare(nd, vk->neg_delta_lines);
   if (!vk->beta.inf) g2_prepare(vk->beta, vk->beta_lines);
-  for (int i = 0; i < raw.n_ic; i++) g1_shift_table(vk->ic[i], vk->ic_sh[i]);
-  g1_shift_table(vk->alpha, vk->alpha_sh);
   vk->loaded = 1;
   return 0;
 }

@@ -329,8 +329,10 @@ struct NodeBufs {
   int m;
 };
 
-// VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k, each 255-bit scalar
-// split into 8 x 32-bit chunks against the pre-shifted bases [2^(32 w)] base (8 threads).
+// VK-side small MSM per checked node: S_kj ic_k[j] and (-S_k0) alpha_k (merged keys: ONE
+// alpha term -(sum_k S_k0) alpha, on key 0's slot), each 255-bit scalar as 32 byte-digits
+// against the key's comb tables; lane w of the scalar's 8 sums the table points of bytes
+// 4w .. 4w + 3 (4 mixed additions, no doublings).
 __global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb, const int* gate) {
   if (gate && *gate == 0) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -342,17 +344,61 @@ __global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb, const
   const int node = nb.nodes[idx];
   const DevVK& vk = b.vks[kind];
   G1J res = jac_infinity<Fq>();
+  bool live = false;
+  uint32_t limb = 0;
   if (vk.loaded) {
     const Fr* s = b.stree + (node * ZG_NKINDS + kind) * ZG_MAX_IC;
-    if (j < vk.ic_len) {
-      Fr sc = fr_from_mont(s[j]);
-      res = jac_mul_limbs(vk.ic_sh[j][w], &sc.l[w], 32);
-    } else if (j == ZG_MAX_IC && !vk.alpha.inf) {
-      Fr sc = fr_from_mont(fp_neg<FrM>(s[0]));
-      res = jac_mul_limbs(vk.alpha_sh[w], &sc.l[w], 32);
+    if (j < vk.ic_len && !vk.ic[j].inf) {
+      live = true;
+      limb = fr_from_mont(s[j]).l[w];
+    } else if (j == ZG_MAX_IC && !vk.alpha.inf && (!b.merged || kind == 0)) {
+      Fr s0 = s[0];
+      if (b.merged)
+        for (int k = 1; k < ZG_NKINDS; k++) s0 = fr_add(s0, b.stree[(node * ZG_NKINDS + k) * ZG_MAX_IC]);
+      live = true;
+      limb = fr_from_mont(fp_neg<FrM>(s0)).l[w];
+    }
+  }
+  if (live) {
+    const uint32_t* tab = vk.comb + (size_t)j * ZG_COMB_W * ZG_COMB_D * ZG_COMB_WORDS;
+    for (int q = 0; q < 4; q++) {
+      const uint32_t d = (limb >> (8 * q)) & 0xffu;
+      if (!d) continue;
+      const uint32_t* e = tab + ((size_t)(4 * w + q) * ZG_COMB_D + (d - 1)) * ZG_COMB_WORDS;
+      G1A p;
+      for (int l = 0; l < 12; l++) {
+        p.x.l[l] = e[l];
+        p.y.l[l] = e[12 + l];
+      }
+      p.inf = false;
+      res = jac_add_aff_inl(res, p);
     }
   }
   nb.msm[t] = res;
+}
+
+// the comb tables of one key: lane per (base, window w, digit d) -> d * 2^(8 w) * base (affine)
+__global__ void __launch_bounds__(64) k_vk_comb(const DevVK* vkp, uint32_t* table) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ZG_COMB_POINTS) return;
+  const DevVK& vk = *vkp;
+  const int d = t % ZG_COMB_D + 1, w = (t / ZG_COMB_D) % ZG_COMB_W, base = t / (ZG_COMB_D * ZG_COMB_W);
+  G1A p;
+  p.inf = true;
+  if (base < vk.ic_len)
+    p = vk.ic[base];
+  else if (base == ZG_MAX_IC)
+    p = vk.alpha;
+  uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int bit = 8 * w;
+  k[bit >> 5] = (uint32_t)d << (bit & 31);
+  if ((bit & 31) > 24) k[(bit >> 5) + 1] = (uint32_t)d >> (32 - (bit & 31));
+  G1A r = p.inf ? p : jac_to_aff(jac_mul_limbs(p, k, 256));
+  uint32_t* e = table + (size_t)t * ZG_COMB_WORDS;
+  for (int l = 0; l < 12; l++) {  // an infinite base / multiple is never looked up (ic[j].inf, alpha.inf)
+    e[l] = r.inf ? 0u : r.x.l[l];
+    e[12 + l] = r.inf ? 0u : r.y.l[l];
+  }
 }
 
 // slot[dst] = the sparse line c2 + (c1 px) v + (c0 py) v w as an Fq12 (pairing `ell` operand)
@@ -389,59 +435,72 @@ __device__ void coop_miller_prepared(CoopWS* ws, const Fq& px, const Fq& py, con
   coop_conj(ws, 0, 0);
 }
 
-// VK-side Miller loops per checked node: one wave per (node, kind, pair)
+// VK-side Miller loops per checked node: one wave per (node, pair slot), ZG_NODE_PAIRS or
+// ZG_NODE_PAIRS_MERGED slots per node (zg_batch.h)
 __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb, const int* gate) {
   if (gate && *gate == 0) return;
   __shared__ CoopWS ws;
   __shared__ Fq px, py;
   __shared__ const Line* lines;
+  const int npn = b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS;
   const int t = blockIdx.x;
-  if (t >= nb.m * ZG_NKINDS * ZG_NPAIRS) return;
+  if (t >= nb.m * npn) return;
   coop_init(&ws);
-  const int idx = t / (ZG_NKINDS * ZG_NPAIRS);
-  const int kind = (t / ZG_NPAIRS) % ZG_NKINDS;
-  const int pair = t % ZG_NPAIRS;
-  const int node = nb.nodes[idx];
-  const DevVK& vk = b.vks[kind];
-  // the G1 point of this pair: the sum of up to 80 MSM partials (gamma pair), 8 (beta pair) or
-  // the batch's C sum (delta pair) -- summed across the wave (one add per lane + 6 LDS levels)
-  __shared__ G1J red[64];
-  const int lane = threadIdx.x & 63;
-  const G1J* ms = nb.msm + (size_t)(idx * ZG_NKINDS + kind) * ZG_MSM_SLOTS * ZG_SHIFTS;
-  int cnt = 0, off = 0;
-  const Line* ln = nullptr;
-  if (vk.loaded) {
-    if (pair == 0 && !vk.gamma.inf) {
-      cnt = vk.ic_len * ZG_SHIFTS;
-      ln = vk.neg_gamma_lines;
-    } else if (pair == 1 && !vk.delta.inf) {
-      ln = vk.neg_delta_lines;
-    } else if (pair == 2 && !vk.beta.inf) {
-      cnt = ZG_SHIFTS;
-      off = ZG_MAX_IC * ZG_SHIFTS;
-      ln = vk.beta_lines;
-    }
-  }
-  G1J acc = jac_infinity<Fq>();
-  if (pair == 1) {
-    if (lane == 0) acc = b.ctree[node * ZG_NKINDS + kind];
+  const int idx = t / npn, p = t % npn;
+  // role: 0 gamma, 1 delta, 2 beta; kinds [k0, k1) whose MSM partials form the G1 point
+  int role, k0, k1;
+  if (b.merged) {
+    role = p == 0 ? 0 : p == npn - 1 ? 2 : 1;
+    k0 = role == 1 ? p - 1 : 0;
+    k1 = role == 0 ? ZG_NKINDS : k0 + 1;
   } else {
-    if (lane < cnt) acc = ms[off + lane];
-    if (lane + 64 < cnt) acc = jac_add(acc, ms[off + lane + 64]);
+    role = p % ZG_NPAIRS;
+    k0 = p / ZG_NPAIRS;
+    k1 = k0 + 1;
+  }
+  const int node = nb.nodes[idx];
+  const DevVK& vk0 = b.vks[k0];  // (merged: gamma / alpha / beta are the same in every loaded key)
+  // the G1 point of this pair: the sum of the keys' MSM partials (gamma pair: up to 3 x 10 x 8,
+  // beta pair: 8), or the node's C sum (delta pair), summed across the wave (a few adds per lane
+  // + 6 LDS levels). The reduction borrows the engine's Fq12 slots and op workspace (untouched
+  // by coop_init, set before the Miller loop reads them): 19.4 KB of LDS per wave, so eight
+  // waves per CU fit (the VGPR limit) when a bisection round checks hundreds of nodes.
+  static_assert(sizeof(G1J) * 64 <= offsetof(CoopWS, forms), "reduction scratch inside the workspace");
+  G1J* red = reinterpret_cast<G1J*>(&ws);
+  const int lane = threadIdx.x & 63;
+  const Line* ln = nullptr;
+  G1J acc = jac_infinity<Fq>();
+  if (role == 1) {
+    if (vk0.loaded && !vk0.delta.inf) {
+      ln = vk0.neg_delta_lines;
+      if (lane == 0) acc = b.ctree[node * ZG_NKINDS + k0];
+    }
+  } else {
+    for (int k = k0; k < k1; k++) {
+      const DevVK& vk = b.vks[k];
+      if (!vk.loaded) continue;
+      if (role == 0 && vk.gamma.inf) continue;
+      if (role == 2 && vk.beta.inf) continue;
+      if (!ln) ln = role == 0 ? vk.neg_gamma_lines : vk.beta_lines;
+      const G1J* ms = nb.msm + (size_t)(idx * ZG_NKINDS + k) * ZG_MSM_SLOTS * ZG_SHIFTS;
+      const int cnt = role == 0 ? vk.ic_len * ZG_SHIFTS : ZG_SHIFTS;
+      const int off = role == 0 ? 0 : ZG_MAX_IC * ZG_SHIFTS;
+      for (int q = lane; q < cnt; q += 64) acc = jac_add_full(acc, ms[off + q]);
+    }
   }
   red[lane] = acc;
   __syncthreads();
   for (int s = 32; s >= 1; s >>= 1) {
-    if (lane < s) red[lane] = jac_add(red[lane], red[lane + s]);
+    if (lane < s) red[lane] = jac_add_full(red[lane], red[lane + s]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     lines = nullptr;
     if (ln) {
-      G1A p = jac_to_aff(red[0]);
-      if (!p.inf) {
-        px = p.x;
-        py = p.y;
+      G1A pa = jac_to_aff(red[0]);
+      if (!pa.inf) {
+        px = pa.x;
+        py = pa.y;
         lines = ln;
       }
     }
@@ -452,7 +511,7 @@ __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb, con
   } else {
     coop_set_one(&ws, 0);
   }
-  coop_store(&ws, 0, nb.pairf[t]);
+  coop_store(&ws, 0, nb.pairf[(size_t)idx * ZG_NODE_PAIRS + p]);
 }
 
 // One wave per node (lane-cooperative Fq12 engine, zg_coop.h).
@@ -464,12 +523,13 @@ __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int
   if (idx >= nb.m) return;
   coop_init(&ws);
   coop_load(&ws, 0, b.ftree[nb.nodes[idx]]);
-  for (int k = 0; k < ZG_NKINDS; k++)
-    for (int p = 0; p < ZG_NPAIRS; p++) {
-      if (mode == 2 && p == 2) continue;
-      coop_load(&ws, 1, nb.pairf[(idx * ZG_NKINDS + k) * ZG_NPAIRS + p]);
-      coop_mul(&ws, 0, 0, 1);
-    }
+  const int npn = b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS;
+  for (int p = 0; p < npn; p++) {
+    const bool beta = b.merged ? p == npn - 1 : p % ZG_NPAIRS == 2;
+    if (mode == 2 && beta) continue;
+    coop_load(&ws, 1, nb.pairf[(size_t)idx * ZG_NODE_PAIRS + p]);
+    coop_mul(&ws, 0, 0, 1);
+  }
   if (mode == 1) {
     coop_store(&ws, 0, nb.out[idx]);
     return;
@@ -505,9 +565,9 @@ __global__ void __launch_bounds__(64) k_f12_from_bytes(const uint8_t* in, int co
 }
 
 // prepare_verifying_key (one thread)
-__global__ void __launch_bounds__(64) k_vk_prepare(const RawVK* raw, DevVK* vk, int* err) {
+__global__ void __launch_bounds__(64) k_vk_prepare(const RawVK* raw, DevVK* vk, int* err, const uint32_t* comb) {
   if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
-  *err = vk_prepare(*raw, vk);
+  *err = vk_prepare(*raw, vk, comb);
 }
 
 // bellman-exact single-proof verification (K-per-proof; parity path and leaf checks)
