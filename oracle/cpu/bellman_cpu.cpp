@@ -111,7 +111,49 @@ static inline Fq mul(const Fq& a, const Fq& b) {  // CIOS
   if (t[6] || geq_p(r.v)) sub_p(r.v);
   return r;
 }
-static inline Fq sqr(const Fq& a) { return mul(a, a); }
+// pairing 0.14 Fq::square: the 15 off-diagonal limb products once, doubled, plus the 6
+// squares, then the Montgomery reduction of the 12-limb value
+static inline Fq sqr(const Fq& a) {
+  uint64_t t[12] = {0};
+  for (int i = 0; i < 5; i++) {
+    uint64_t c = 0;
+    for (int j = i + 1; j < 6; j++) {
+      u128 s = (u128)a.v[i] * a.v[j] + t[i + j] + c;
+      t[i + j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    t[i + 6] = c;
+  }
+  t[11] = t[10] >> 63;
+  for (int i = 10; i >= 1; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 63);
+  t[0] <<= 1;
+  uint64_t c = 0;
+  for (int i = 0; i < 6; i++) {
+    u128 s = (u128)a.v[i] * a.v[i] + t[2 * i] + c;
+    t[2 * i] = (uint64_t)s;
+    u128 s2 = (u128)t[2 * i + 1] + (uint64_t)(s >> 64);
+    t[2 * i + 1] = (uint64_t)s2;
+    c = (uint64_t)(s2 >> 64);
+  }
+  // mont_reduce: t[0..12) * 2^-384 mod p
+  uint64_t carry2 = 0;
+  for (int i = 0; i < 6; i++) {
+    const uint64_t k = t[i] * PINV;
+    uint64_t cc = 0;
+    for (int j = 0; j < 6; j++) {
+      u128 s = (u128)k * P[j] + t[i + j] + cc;
+      t[i + j] = (uint64_t)s;
+      cc = (uint64_t)(s >> 64);
+    }
+    u128 s = (u128)t[i + 6] + cc + carry2;
+    t[i + 6] = (uint64_t)s;
+    carry2 = (uint64_t)(s >> 64);
+  }
+  Fq r;
+  memcpy(r.v, t + 6, 48);
+  if (carry2 || geq_p(r.v)) sub_p(r.v);
+  return r;
+}
 static inline bool is_zero(const Fq& a) { return !(a.v[0] | a.v[1] | a.v[2] | a.v[3] | a.v[4] | a.v[5]); }
 static inline bool eq(const Fq& a, const Fq& b) { return !memcmp(a.v, b.v, 48); }
 static Fq one() {
@@ -156,7 +198,71 @@ static void init_exps() {
   t[0] -= 1;
   for (int i = 0; i < 6; i++) EXP_HALF[i] = (t[i] >> 1) | (i < 5 ? t[i + 1] << 63 : 0);
 }
-static Fq inv(const Fq& a) { return pow_limbs(a, EXP_INV, 381); }
+// pairing 0.14 Fq::inverse: binary extended Euclid on the Montgomery representation
+// (Guide to Pairing-based Cryptography, Algorithm 16): u = aR, b = R^2 -> b = a^-1 R
+static inline bool is_one_raw(const uint64_t* u) { return u[0] == 1 && !(u[1] | u[2] | u[3] | u[4] | u[5]); }
+static inline void shr1(uint64_t* u) {
+  for (int i = 0; i < 5; i++) u[i] = (u[i] >> 1) | (u[i + 1] << 63);
+  u[5] >>= 1;
+}
+static inline bool lt_raw(const uint64_t* a, const uint64_t* b) {
+  for (int i = 5; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] < b[i];
+  }
+  return false;
+}
+static inline void sub_raw(uint64_t* a, const uint64_t* b) {
+  uint64_t br = 0;
+  for (int i = 0; i < 6; i++) {
+    u128 t = (u128)a[i] - b[i] - br;
+    a[i] = (uint64_t)t;
+    br = (uint64_t)(t >> 127);
+  }
+}
+static inline void half_mod(uint64_t* x) {  // x / 2 mod p (x < p)
+  if (x[0] & 1) {
+    uint64_t c = 0;
+    for (int i = 0; i < 6; i++) {
+      u128 t = (u128)x[i] + P[i] + c;
+      x[i] = (uint64_t)t;
+      c = (uint64_t)(t >> 64);
+    }
+  }
+  shr1(x);
+}
+static Fq inv(const Fq& a) {
+  if (is_zero(a)) return a;  // (callers never invert zero: pairing returns None)
+  uint64_t u[6], v[6], b[6], c[6] = {0, 0, 0, 0, 0, 0};
+  memcpy(u, a.v, 48);
+  memcpy(v, P, 48);
+  memcpy(b, R2, 48);
+  while (!is_one_raw(u) && !is_one_raw(v)) {
+    while (!(u[0] & 1)) {
+      shr1(u);
+      half_mod(b);
+    }
+    while (!(v[0] & 1)) {
+      shr1(v);
+      half_mod(c);
+    }
+    if (lt_raw(v, u)) {
+      sub_raw(u, v);
+      Fq x, y;
+      memcpy(x.v, b, 48);
+      memcpy(y.v, c, 48);
+      memcpy(b, sub(x, y).v, 48);
+    } else {
+      sub_raw(v, u);
+      Fq x, y;
+      memcpy(x.v, c, 48);
+      memcpy(y.v, b, 48);
+      memcpy(c, sub(x, y).v, 48);
+    }
+  }
+  Fq r;
+  memcpy(r.v, is_one_raw(u) ? b : c, 48);
+  return r;
+}
 
 // ---------------------------------------------------------------- tower
 struct Fq2 {
