@@ -173,6 +173,27 @@ int zg_prep_joinsplit(const uint8_t anchor[32], const uint8_t random_seed[32], c
 int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32], const uint8_t pubkey[32],
             uint8_t out[32]);
 
+/* ---- Sapling signatures and Jubjub points on the GPU: the checks that sit
+ * next to the Groth16 proofs in accept_sapling, batched. Any n; device memory per call.
+ *   zg_redjubjub_verify <- redjubjub::PublicKey::read + verify (sapling-crypto @21084bde), called at
+ *        verification/src/sapling.rs:124-137 (spend_auth_sig: vk = rk, msg = rk || sighash,
+ *        ZG_GEN_SPEND_AUTH) and :228-238 (binding_sig: vk = bvk, msg = bvk || sighash,
+ *        ZG_GEN_BINDING). vk n x 32, sig n x 64 (Rbar || Sbar), msg n x 64, gen n -> ok n (1 / 0)
+ *   zg_sapling_bvk      <- the binding verification key of each transaction (sapling.rs:82-94,
+ *        216-226, 247-269): sum cv(spends) - sum cv(outputs) - [valueBalance] G_v. cvs: per tx its
+ *        n_spends spend cvs then n_outputs output cvs (32 B each), transactions back to back;
+ *        -> bvk ntx x 32 (edwards::Point::write) and status ntx: 0 ok, 1 a cv does not decode,
+ *        2 valueBalance == INT64_MIN (InvalidBalanceValue)
+ *   zg_jubjub_decode    <- edwards::Point::read + is_small_order (sapling.rs:280-292): status n
+ *        (0 ok, 1 invalid, 2 small order), xy optional n x 64 (x || y canonical LE Fr) */
+#define ZG_GEN_SPEND_AUTH 0 /* FixedGenerators::SpendingKeyGenerator */
+#define ZG_GEN_BINDING 1    /* FixedGenerators::ValueCommitmentRandomness */
+int zg_redjubjub_verify(zg_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                        const uint8_t* gen, uint8_t* ok);
+int zg_sapling_bvk(zg_ctx* ctx, size_t ntx, const uint32_t* n_spends, const uint32_t* n_outputs, const uint8_t* cvs,
+                   const int64_t* value_balance, uint8_t* bvk, uint8_t* status);
+int zg_jubjub_decode(zg_ctx* ctx, size_t n, const uint8_t* points, uint8_t* status, uint8_t* xy);
+
 /* ---- synthetic workload (bench/tests): Groth16 re-randomization of real proofs,
  * out[i] = rerandomize(src[src_index[i]]) with (t, s) = BLAKE2b-512("zg-rerand"||seed||i)
  * (A,B,C) -> (t^-1 A, t B + t s delta, C + s A); valid iff the source is. */

@@ -47,6 +47,9 @@ pub const ZG_INPUT_STRIDE: usize = ZG_MAX_INPUTS * ZG_FR_BYTES;
 pub const ZG_GT_BYTES: usize = 576;
 pub const ZG_R_BYTES: usize = 16;
 
+pub const ZG_GEN_SPEND_AUTH: u8 = 0;
+pub const ZG_GEN_BINDING: u8 = 1;
+
 pub const ZG_PREP_OK: c_int = 0;
 pub const ZG_PREP_VALUE_COMMITMENT_INVALID: c_int = 1;
 pub const ZG_PREP_VALUE_COMMITMENT_SMALL_ORDER: c_int = 2;
@@ -94,6 +97,12 @@ extern "C" {
                              commitments: *const u8, vpub_old: u64, vpub_new: u64, pubkey: *const u8,
                              inputs: *mut u8) -> c_int;
     pub fn zg_hsig(random_seed: *const u8, nf0: *const u8, nf1: *const u8, pubkey: *const u8, out: *mut u8) -> c_int;
+
+    pub fn zg_redjubjub_verify(ctx: *mut ZgCtx, n: usize, vk: *const u8, sig: *const u8, msg: *const u8,
+                               gen: *const u8, ok: *mut u8) -> c_int;
+    pub fn zg_sapling_bvk(ctx: *mut ZgCtx, ntx: usize, n_spends: *const u32, n_outputs: *const u32, cvs: *const u8,
+                          value_balance: *const i64, bvk: *mut u8, status: *mut u8) -> c_int;
+    pub fn zg_jubjub_decode(ctx: *mut ZgCtx, n: usize, points: *const u8, status: *mut u8, xy: *mut u8) -> c_int;
 
     pub fn zg_synth_rerandomize(ctx: *mut ZgCtx, n_src: usize, src_proofs: *const u8, src_kinds: *const u8,
                                 n: usize, src_index: *const u32, seed: u64, out_proofs: *mut u8) -> c_int;

@@ -394,6 +394,117 @@ def gen_vk_codec():
     print("wrote vk_codec.json", len(vecs))
 
 
+def gen_sapling_sigs():
+    """sapling_sigs.json: the RedJubjub checks of accept_sapling on the
+    reference's real Sapling transactions, with the no-input ZIP-243 sighash the acceptor
+    computes (accept_transaction.rs:374-386), plus mutants in the reference's failure classes,
+    a seeded batch of oracle-signed signatures, and a sample of script/data/sighash_tests.json
+    (the official ZIP-143/243 vectors) pinning the sighash restatement."""
+    import random
+    from oracle import sapling_sig as S
+    tx_hex, _, _, block_hex, _ = extract_sources()
+    _, btxs = Z.parse_block_hex(block_hex)
+    raws = [("bd4fe81c", bytes.fromhex(tx_hex))]
+    rd = Z._Reader(bytes.fromhex(block_hex))
+    rd.take(140)
+    rd.take(rd.compact())
+    for _ in range(rd.compact()):
+        o0 = rd.o
+        t = Z.parse_tx(rd)
+        raws.append((t["txid"][:8], rd.d[o0:rd.o]))
+    txs, sigs = [], []
+    for name, raw in raws:
+        t = S.parse_tx_raw(raw)
+        if not (t["spends"] or t["soutputs"]):
+            continue
+        auth, bind, sh = S.sapling_checks(raw)
+        assert all(auth) and bind, name          # consensus-valid / accept_sapling_works
+        e = {"name": name, "sighash": hx(sh), "value_balance": int.from_bytes(t["value_balance"], "little", signed=True),
+             "spend_cvs": [hx(s[0:32]) for s in t["spends"]], "output_cvs": [hx(o[0:32]) for o in t["soutputs"]],
+             "binding_sig": hx(t["binding_sig"]), "binding_ok": True}
+        bvk = S.binding_verification_key([s[0:32] for s in t["spends"]], [o[0:32] for o in t["soutputs"]],
+                                         e["value_balance"])
+        e["bvk"] = hx(S.encode(bvk))
+        txs.append(e)
+        for s in t["spends"]:
+            sigs.append({"name": name + ":spend_auth", "vk": hx(s[96:128]), "sig": hx(s[320:384]),
+                         "msg": hx(s[96:128] + sh), "gen": S.GEN_SPEND_AUTH, "ok": True})
+        sigs.append({"name": name + ":binding", "vk": e["bvk"], "sig": e["binding_sig"],
+                     "msg": hx(S.encode(bvk) + sh), "gen": S.GEN_BINDING, "ok": True})
+    # mutants (verify() -> false unless noted)
+    base = [s for s in sigs if s["name"] == "bd4fe81c:spend_auth"][0]
+    vk, sig, msg = bytes.fromhex(base["vk"]), bytes.fromhex(base["sig"]), bytes.fromhex(base["msg"])
+
+    def mut(name, v, s_, m, gen=S.GEN_SPEND_AUTH, pinned=None):
+        ok = S.redjubjub_verify(v, s_, m, gen)
+        sigs.append({"name": name, "vk": hx(v), "sig": hx(s_), "msg": hx(m), "gen": gen, "ok": ok,
+                     "pinned_by": pinned})
+    mut("zero_sig", vk, bytes(64), msg, pinned="verification/src/sapling.rs:414-419 (BadSpendAuthSig)")
+    mut("msg_bitflip", vk, sig, bytes([msg[0] ^ 1]) + msg[1:])
+    mut("sighash_bitflip", vk, sig, msg[:40] + bytes([msg[40] ^ 0x80]) + msg[41:])
+    mut("wrong_generator", vk, sig, msg, gen=S.GEN_BINDING)
+    s_int = int.from_bytes(sig[32:], "little")
+    mut("S_plus_rJ", vk, sig[:32] + (s_int + S.RJ).to_bytes(32, "little"), msg)
+    mut("S_all_ff", vk, sig[:32] + b"\xff" * 32, msg)
+    mut("R_swapped_halves", vk, sig[16:32] + sig[:16] + sig[32:], msg)
+    mut("R_y_ge_q", vk, (S.R + 1).to_bytes(32, "little") + sig[32:], msg)
+    mut("R_sign_flipped", vk, sig[:31] + bytes([sig[31] ^ 0x80]) + sig[32:], msg)
+    mut("vk_swapped_halves", vk[16:] + vk[:16], sig, msg)
+    mut("vk_small_order", bytes(32), sig, msg)
+    mut("vk_identity", (1).to_bytes(32, "little"), sig, msg)
+    mut("S_zero", vk, sig[:32] + bytes(32), msg)
+    mut("R_zero_point", vk, (1).to_bytes(32, "little") + sig[32:], msg)
+    # a small-order component added to R is killed by the cofactor: still VALID (h_G = 8)
+    rpt = S.read(sig[:32])
+    t2 = S.read((S.R - 1).to_bytes(32, "little"))     # (0, -1): order 2
+    mut("R_plus_order2", vk, S.encode(S.add(rpt, t2)) + sig[32:], msg)
+    # binding-signature failures (accept_sapling_final_fails, sapling.rs:512-530)
+    tb = txs[0]
+    bsig = bytes.fromhex(tb["binding_sig"])
+    sh = bytes.fromhex(tb["sighash"])
+    zero_bvk = S.ZERO
+    sigs.append({"name": "bd4fe81c:binding_total_zero", "vk": hx(S.encode(S.neg(S.value_balance_point(tb["value_balance"])))),
+                 "sig": hx(bsig), "msg": hx(S.encode(S.neg(S.value_balance_point(tb["value_balance"]))) + sh),
+                 "gen": S.GEN_BINDING, "ok": False, "pinned_by": "verification/src/sapling.rs:525-529 (BadBindingSignature)"})
+    assert not S.redjubjub_verify(bytes.fromhex(sigs[-1]["vk"]), bsig, bytes.fromhex(sigs[-1]["msg"]), S.GEN_BINDING)
+    assert zero_bvk is not None
+    for s in sigs:
+        if s.get("pinned_by"):
+            assert s["ok"] is False, s["name"]
+    # oracle-signed batch (seeded): valid signatures under random keys and messages
+    rng = random.Random(7)
+    batch = []
+    for i in range(48):
+        gen = i % 2
+        sk = rng.randrange(1, S.RJ)
+        m = rng.randbytes(64)
+        sg = S.redjubjub_sign(sk, m, gen, rng.randbytes(80))
+        batch.append({"vk": hx(S.public_key(sk, gen)), "sig": hx(sg), "msg": hx(m), "gen": gen, "ok": True})
+        assert S.redjubjub_verify(bytes.fromhex(batch[-1]["vk"]), sg, m, gen)
+    # ZIP-143/243 vectors (overwintered transactions), a spread sample
+    vecs = json.load(open(os.path.join(REF, "script/data/sighash_tests.json")))[1:]
+    sample = []
+    for v in vecs:
+        t = S.parse_tx_raw(bytes.fromhex(v[0]))
+        if not t["overwintered"]:
+            continue
+        ii = None if v[2] == (1 << 64) - 1 else v[2]
+        got = S.sighash(t, ii, bytes.fromhex(v[1]), 0, v[3] & 0xFFFFFFFF, v[4])
+        assert got == bytes.fromhex(v[5])[::-1]
+        if len(sample) < 48 and len(v[0]) < 6000:
+            sample.append({"tx": v[0], "script": v[1], "input_index": ii, "hashtype": v[3] & 0xFFFFFFFF,
+                           "branch_id": v[4], "sighash": hx(got)})
+    gens = {"spending_key": hx(S.encode(S.SPENDING_KEY_GENERATOR)),
+            "value_commitment_value": hx(S.encode(S.VALUE_COMMITMENT_VALUE)),
+            "value_commitment_randomness": hx(S.encode(S.VALUE_COMMITMENT_RANDOMNESS))}
+    with open(os.path.join(HERE, "sapling_sigs.json"), "w") as f:
+        json.dump({"generators": gens, "txs": txs, "sigs": sigs, "signed_batch": batch, "sighash_vectors": sample,
+                   "source": "oracle/sapling_sig.py on the reference's transactions (sapling.rs:303-305, "
+                             "test-data/src/lib.rs:117-131) and script/data/sighash_tests.json"},
+                  f, indent=1, sort_keys=True)
+    print("wrote sapling_sigs.json", len(txs), "txs", len(sigs), "sigs", len(sample), "sighash vectors")
+
+
 def refresh_batch_gt():
     """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
     change of the batch-scalar mapping; no reference sources needed)"""
@@ -417,5 +528,7 @@ if __name__ == "__main__":
         refresh_batch_gt()
     elif len(sys.argv) > 1 and sys.argv[1] == "--vk-codec":
         gen_vk_codec()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--sapling-sigs":
+        gen_sapling_sigs()
     else:
         main()

@@ -55,6 +55,7 @@ struct zg_dev {
     int err = 0;
   };
   std::vector<VKEntry*> vks;  // prepare_verifying_key once per distinct key per device
+  uint32_t* jj_comb = nullptr;  // Jubjub generators' comb tables (zg_jubjub.h), built on first use
 };
 
 static std::mutex g_devs_mu;
@@ -154,6 +155,7 @@ static void dev_release(zg_dev* d) {
     if (e->comb) hipFree(e->comb);
     delete e;
   }
+  if (d->jj_comb) hipFree(d->jj_comb);
   g_devs[d->device] = nullptr;
   delete d;
 }
@@ -616,6 +618,13 @@ hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs&
 hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate,
                            hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr);          // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
+hipError_t launch_jj_comb(hipStream_t st, uint32_t* table);                                    // zg_jubjub.hip
+hipError_t launch_redjubjub(hipStream_t st, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                            const uint8_t* gen, int n, const uint32_t* comb, uint8_t* ok);
+hipError_t launch_jj_decode(hipStream_t st, const uint8_t* pts, int n, uint8_t* status, uint8_t* xy);
+hipError_t launch_sapling_bvk(hipStream_t st, int ntx, const uint32_t* off, const uint32_t* nspends,
+                              const uint8_t* cvs, const int64_t* vb, const uint32_t* comb, uint8_t* bvk,
+                              uint8_t* status);
 }
 
 // The pipeline on device-resident inputs already in ctx buffers.
@@ -1038,6 +1047,122 @@ extern "C" int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n) {
   if (!ctx || (n && !out)) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   for (size_t i = 0; i < n; i++) out[i] = i < ZG_NSTATS ? ctx->stats[i] : 0;
+  return ZG_OK;
+}
+
+// ------------------------------------------------------------------ Sapling signatures (zg_jubjub.h)
+#define ZG_JJ_COMB_BYTES (sizeof(uint32_t) * 16 * (size_t)(3 * 32 * 255))
+static int jj_comb(zg_ctx* ctx, const uint32_t** out) {
+  zg_dev* d = ctx->dev;
+  std::lock_guard<std::mutex> g(d->mu);
+  if (!d->jj_comb) {
+    uint32_t* t = nullptr;
+    HIPCHK(hipMalloc(&t, ZG_JJ_COMB_BYTES));
+    hipError_t e = launch_jj_comb(ctx->stream, t);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      hipFree(t);
+      return fail(ctx, ZG_E_HIP, std::string("Jubjub comb tables: ") + hipGetErrorString(e));
+    }
+    d->jj_comb = t;
+  }
+  *out = d->jj_comb;
+  return ZG_OK;
+}
+
+// device buffers of one call, freed on every path
+struct DevScratch {
+  std::vector<void*> p;
+  ~DevScratch() {
+    for (void* q : p) hipFree(q);
+  }
+  template <class T>
+  hipError_t alloc(T** x, size_t bytes) {
+    hipError_t e = hipMalloc((void**)x, bytes ? bytes : 1);
+    if (e == hipSuccess) p.push_back(*x);
+    return e;
+  }
+};
+
+extern "C" int zg_redjubjub_verify(zg_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                                   const uint8_t* gen, uint8_t* ok) {
+  if (!ctx || (n && (!vk || !sig || !msg || !gen || !ok)) || n > (1u << 30)) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!n) return ZG_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  const uint32_t* comb = nullptr;
+  int rc = jj_comb(ctx, &comb);
+  if (rc) return rc;
+  DevScratch s;
+  uint8_t *dvk, *dsig, *dmsg, *dgen, *dok;
+  HIPCHK(s.alloc(&dvk, 32 * n));
+  HIPCHK(s.alloc(&dsig, 64 * n));
+  HIPCHK(s.alloc(&dmsg, 64 * n));
+  HIPCHK(s.alloc(&dgen, n));
+  HIPCHK(s.alloc(&dok, n));
+  HIPCHK(hipMemcpyAsync(dvk, vk, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(dsig, sig, 64 * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(dmsg, msg, 64 * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(dgen, gen, n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(launch_redjubjub(ctx->stream, dvk, dsig, dmsg, dgen, (int)n, comb, dok));
+  HIPCHK(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+extern "C" int zg_sapling_bvk(zg_ctx* ctx, size_t ntx, const uint32_t* n_spends, const uint32_t* n_outputs,
+                              const uint8_t* cvs, const int64_t* value_balance, uint8_t* bvk, uint8_t* status) {
+  if (!ctx || (ntx && (!n_spends || !n_outputs || !value_balance || !bvk || !status)) || ntx > (1u << 30))
+    return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ntx) return ZG_OK;
+  std::vector<uint32_t> off(ntx + 1, 0);
+  for (size_t t = 0; t < ntx; t++) {
+    const uint64_t next = (uint64_t)off[t] + n_spends[t] + n_outputs[t];
+    if (next > (1u << 30)) return fail(ctx, ZG_E_INVAL, "too many value commitments");
+    off[t + 1] = (uint32_t)next;
+  }
+  if (off[ntx] && !cvs) return ZG_E_INVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  const uint32_t* comb = nullptr;
+  int rc = jj_comb(ctx, &comb);
+  if (rc) return rc;
+  DevScratch s;
+  uint32_t *doff, *dns;
+  uint8_t *dcv, *dbvk, *dst;
+  int64_t* dvb;
+  HIPCHK(s.alloc(&doff, sizeof(uint32_t) * (ntx + 1)));
+  HIPCHK(s.alloc(&dns, sizeof(uint32_t) * ntx));
+  HIPCHK(s.alloc(&dcv, (size_t)32 * off[ntx]));
+  HIPCHK(s.alloc(&dvb, sizeof(int64_t) * ntx));
+  HIPCHK(s.alloc(&dbvk, 32 * ntx));
+  HIPCHK(s.alloc(&dst, ntx));
+  HIPCHK(hipMemcpyAsync(doff, off.data(), sizeof(uint32_t) * (ntx + 1), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(dns, n_spends, sizeof(uint32_t) * ntx, hipMemcpyHostToDevice, ctx->stream));
+  if (off[ntx]) HIPCHK(hipMemcpyAsync(dcv, cvs, (size_t)32 * off[ntx], hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(dvb, value_balance, sizeof(int64_t) * ntx, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(launch_sapling_bvk(ctx->stream, (int)ntx, doff, dns, dcv, dvb, comb, dbvk, dst));
+  HIPCHK(hipMemcpyAsync(bvk, dbvk, 32 * ntx, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(status, dst, ntx, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return ZG_OK;
+}
+
+extern "C" int zg_jubjub_decode(zg_ctx* ctx, size_t n, const uint8_t* points, uint8_t* status, uint8_t* xy) {
+  if (!ctx || (n && (!points || !status)) || n > (1u << 30)) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!n) return ZG_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  DevScratch s;
+  uint8_t *dp, *dst, *dxy = nullptr;
+  HIPCHK(s.alloc(&dp, 32 * n));
+  HIPCHK(s.alloc(&dst, n));
+  if (xy) HIPCHK(s.alloc(&dxy, 64 * n));
+  HIPCHK(hipMemcpyAsync(dp, points, 32 * n, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(launch_jj_decode(ctx->stream, dp, (int)n, dst, dxy));
+  HIPCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, ctx->stream));
+  if (xy) HIPCHK(hipMemcpyAsync(xy, dxy, 64 * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   return ZG_OK;
 }
 

@@ -169,23 +169,25 @@ __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const 
 }
 
 // root Fr sums from the stree leaves (decode_finish: r_i, r_i x_ij in the proof's kind, zero
-// elsewhere): block (kind * 10 + slot, chunk) sums ZG_FR_CHUNK leaves
-__global__ void __launch_bounds__(256) k_fr_root(BatchBufs b, MsmBufs m, const int* gate) {
+// elsewhere): block `chunk` sums ZG_FR_CHUNK leaves for all 30 (kind, slot) sums at once --
+// lanes t = 30 g + ks read a leaf's 30 consecutive Fr (960 contiguous bytes per 30 lanes), so
+// every leaf byte is fetched once
+#define ZG_FR_G 8
+__global__ void __launch_bounds__(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G) k_fr_root(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  __shared__ Fr sh[256];
-  const int ks = blockIdx.x, chunk = blockIdx.y, t = threadIdx.x;
-  const int kind = ks / ZG_MAX_IC, slot = ks % ZG_MAX_IC;
+  constexpr int KS = ZG_NKINDS * ZG_MAX_IC;
+  __shared__ Fr sh[KS * ZG_FR_G];
+  const int chunk = blockIdx.x, t = threadIdx.x, ks = t % KS, g = t / KS;
   Fr acc = fp_zero<FrM>();
   const int lo = chunk * ZG_FR_CHUNK, hi = min(lo + ZG_FR_CHUNK, b.npad);
-  for (int i = lo + t; i < hi; i += 256)
-    acc = fr_add(acc, b.stree[((size_t)(b.npad + i) * ZG_NKINDS + kind) * ZG_MAX_IC + slot]);
+  for (int i = lo + g; i < hi; i += ZG_FR_G) acc = fr_add(acc, b.stree[(size_t)(b.npad + i) * KS + ks]);
   sh[t] = acc;
   __syncthreads();
-  for (int s = 128; s >= 1; s >>= 1) {
-    if (t < s) sh[t] = fr_add(sh[t], sh[t + s]);
+  for (int s = ZG_FR_G / 2; s >= 1; s >>= 1) {
+    if (g < s) sh[t] = fr_add(sh[t], sh[t + s * KS]);
     __syncthreads();
   }
-  if (t == 0) m.frpart[(size_t)chunk * ZG_NKINDS * ZG_MAX_IC + ks] = sh[0];
+  if (g == 0) m.frpart[(size_t)chunk * KS + ks] = sh[t];
 }
 
 __global__ void __launch_bounds__(64) k_fr_final(BatchBufs b, MsmBufs m, int nchunks, const int* gate) {
@@ -231,7 +233,7 @@ hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m,
   hipLaunchKernelGGL(k_msm_window, dim3(ZG_MSM_GROUPS), dim3(ZG_MSM_WT), 0, st, m, gate);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, b, m, gate);
   const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;
-  hipLaunchKernelGGL(k_fr_root, dim3(ZG_NKINDS * ZG_MAX_IC, nchunks), dim3(256), 0, st, b, m, gate);
+  hipLaunchKernelGGL(k_fr_root, dim3(nchunks), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, gate);
   hipLaunchKernelGGL(k_fr_final, dim3(1), dim3(64), 0, st, b, m, nchunks, gate);
   return hipGetLastError();
 }

@@ -34,16 +34,16 @@ enum : int {
 };
 
 // ---- Fr helpers (host; Montgomery form unless noted)
-inline Fr prep_fr_const(const uint32_t* c) {
+ZG_HD inline Fr prep_fr_const(const uint32_t* c) {
   Fr r;
   for (int i = 0; i < 8; i++) r.l[i] = c[i];
   return r;
 }
-inline Fr prep_fr_sqr(const Fr& a) { return fr_mul(a, a); }
-inline Fr prep_fr_sub(const Fr& a, const Fr& b) { return fp_sub<FrM>(a, b); }
-inline Fr prep_fr_neg(const Fr& a) { return fp_neg<FrM>(a); }
-inline bool prep_fr_eq(const Fr& a, const Fr& b) { return fp_eq<FrM>(a, b); }
-inline Fr prep_fr_pow(const Fr& a, const uint32_t* e, int nbits) {
+ZG_HD inline Fr prep_fr_sqr(const Fr& a) { return fr_mul(a, a); }
+ZG_HD inline Fr prep_fr_sub(const Fr& a, const Fr& b) { return fp_sub<FrM>(a, b); }
+ZG_HD inline Fr prep_fr_neg(const Fr& a) { return fp_neg<FrM>(a); }
+ZG_HD inline bool prep_fr_eq(const Fr& a, const Fr& b) { return fp_eq<FrM>(a, b); }
+ZG_HD inline Fr prep_fr_pow(const Fr& a, const uint32_t* e, int nbits) {
   Fr r = fr_one();
   for (int i = nbits - 1; i >= 0; i--) {
     r = prep_fr_sqr(r);
@@ -51,11 +51,11 @@ inline Fr prep_fr_pow(const Fr& a, const uint32_t* e, int nbits) {
   }
   return r;
 }
-inline Fr prep_fr_inv(const Fr& a) { return prep_fr_pow(a, FR_EXP_INV, 255); }
+ZG_HD inline Fr prep_fr_inv(const Fr& a) { return prep_fr_pow(a, FR_EXP_INV, 255); }
 
 // Tonelli-Shanks (r - 1 = 2^32 t); returns false for a non-residue. Any root: the caller fixes
 // the sign from the encoding.
-inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
+ZG_HD inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
   if (fp_is_zero<FrM>(a)) {
     *out = a;
     return true;
@@ -87,11 +87,11 @@ inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
 }
 
 // 32 little-endian bytes -> canonical Fr limbs; false if >= r
-inline bool prep_fr_from_repr(const uint8_t* b, Fr* canon) {
+ZG_HD inline bool prep_fr_from_repr(const uint8_t* b, Fr* canon) {
   *canon = fr_limbs_from_le(b);
   return fp_lt_modulus<FrM>(*canon);
 }
-inline void prep_fr_to_le(const Fr& canon, uint8_t* b) {
+ZG_HD inline void prep_fr_to_le(const Fr& canon, uint8_t* b) {
   for (int i = 0; i < 8; i++)
     for (int k = 0; k < 4; k++) b[4 * i + k] = (uint8_t)(canon.l[i] >> (8 * k));
 }
@@ -101,7 +101,7 @@ struct JubjubPt {
 };
 
 // edwards::Point::read; false = Invalid
-inline bool jubjub_read(const uint8_t* in, JubjubPt* p) {
+ZG_HD inline bool jubjub_read(const uint8_t* in, JubjubPt* p) {
   uint8_t b[32];
   memcpy(b, in, 32);
   const bool sign = b[31] >> 7;
@@ -122,7 +122,7 @@ inline bool jubjub_read(const uint8_t* in, JubjubPt* p) {
 }
 
 // 8P == identity, in projective (X : Y : Z) with dbl-2008-bbjlp (a = -1)
-inline bool jubjub_is_small_order(const JubjubPt& p) {
+ZG_HD inline bool jubjub_is_small_order(const JubjubPt& p) {
   Fr X = p.x, Y = p.y, Z = fr_one();
   for (int r = 0; r < 3; r++) {
     const Fr B = prep_fr_sqr(fr_add(X, Y));
@@ -140,15 +140,15 @@ inline bool jubjub_is_small_order(const JubjubPt& p) {
 }
 
 // require_non_small_order_point: 0 ok, 1 invalid, 2 small order
-inline int jubjub_read_checked(const uint8_t* b, JubjubPt* p) {
+ZG_HD inline int jubjub_read_checked(const uint8_t* b, JubjubPt* p) {
   if (!jubjub_read(b, p)) return 1;
   return jubjub_is_small_order(*p) ? 2 : 0;
 }
 
-inline void prep_put(uint8_t* out, int j, const Fr& mont) { prep_fr_to_le(fr_from_mont(mont), out + 32 * j); }
+ZG_HD inline void prep_put(uint8_t* out, int j, const Fr& mont) { prep_fr_to_le(fr_from_mont(mont), out + 32 * j); }
 
 // multipack of a 32-byte LE value with CAPACITY 254 (sapling.rs:140-142): low 254 bits, then the top 2
-inline void prep_multipack_nf(const uint8_t* nf, uint8_t* lo, uint8_t* hi) {
+ZG_HD inline void prep_multipack_nf(const uint8_t* nf, uint8_t* lo, uint8_t* hi) {
   memcpy(lo, nf, 32);
   lo[31] &= 0x3f;
   memset(hi, 0, 32);
@@ -156,7 +156,7 @@ inline void prep_multipack_nf(const uint8_t* nf, uint8_t* lo, uint8_t* hi) {
 }
 
 // accept_spend public input [rk.x, rk.y, cv.x, cv.y, anchor, nf0, nf1]
-inline int prep_spend(const uint8_t* cv, const uint8_t* anchor, const uint8_t* nf, const uint8_t* rk, uint8_t* out) {
+ZG_HD inline int prep_spend(const uint8_t* cv, const uint8_t* anchor, const uint8_t* nf, const uint8_t* rk, uint8_t* out) {
   JubjubPt cvp, rkp;
   const int c = jubjub_read_checked(cv, &cvp);
   if (c == 1) return PREP_VALUE_COMMITMENT_INVALID;
@@ -176,7 +176,7 @@ inline int prep_spend(const uint8_t* cv, const uint8_t* anchor, const uint8_t* n
 }
 
 // accept_output public input [cv.x, cv.y, epk.x, epk.y, cmu]
-inline int prep_output(const uint8_t* cv, const uint8_t* cmu, const uint8_t* epk, uint8_t* out) {
+ZG_HD inline int prep_output(const uint8_t* cv, const uint8_t* cmu, const uint8_t* epk, uint8_t* out) {
   JubjubPt cvp, ep;
   const int c = jubjub_read_checked(cv, &cvp);
   if (c == 1) return PREP_VALUE_COMMITMENT_INVALID;

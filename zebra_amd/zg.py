@@ -9,6 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libzg.so")
 
 KIND_SPEND, KIND_OUTPUT, KIND_SPROUT = 0, 1, 2
+GEN_SPEND_AUTH, GEN_BINDING = 0, 1   # include/zg.h ZG_GEN_*
 KIND_NINPUTS = {KIND_SPEND: 7, KIND_OUTPUT: 5, KIND_SPROUT: 9}
 STATUS_OK, STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "DECODE_INVALID", 2: "MALFORMED_VK", 3: "VERIFY_FAILED", 4: "INPUT_NONCANONICAL"}
@@ -62,6 +63,10 @@ def lib():
         L.zg_bench_mad_rate.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.zg_bench_mad_rate_clock.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.zg_chacha20_blocks.argtypes = [vp, u8p, u8p, ctypes.c_uint32, ctypes.c_size_t, u8p]
+        L.zg_redjubjub_verify.argtypes = [vp, sz, u8p, u8p, u8p, u8p, u8p]
+        L.zg_sapling_bvk.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), u8p,
+                                     ctypes.POINTER(ctypes.c_int64), u8p, u8p]
+        L.zg_jubjub_decode.argtypes = [vp, sz, u8p, u8p, u8p]
         L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
         L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
         L.zg_prep_joinsplit.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
@@ -261,6 +266,37 @@ class Context:
         self._chk(lib().zg_synth_rerandomize(self._p, len(src_kinds), bytes(src_proofs), bytes(src_kinds), n, idx,
                                              seed, out))
         return out.raw[:192 * n]
+
+    # ---- Sapling signatures / Jubjub points on the GPU (include/zg.h zg_redjubjub_verify, ...)
+    def redjubjub_verify(self, vks, sigs, msgs, gens):
+        """per item: redjubjub PublicKey::read(vk) + verify(msg, sig, generator) -> list of bool"""
+        n = len(vks)
+        assert len(sigs) == len(msgs) == len(gens) == n
+        ok = ctypes.create_string_buffer(max(n, 1))
+        self._chk(lib().zg_redjubjub_verify(self._p, n, b"".join(map(bytes, vks)), b"".join(map(bytes, sigs)),
+                                            b"".join(map(bytes, msgs)), bytes(gens), ok))
+        return [b == 1 for b in ok.raw[:n]]
+
+    def sapling_bvk(self, txs):
+        """txs: list of (spend cvs, output cvs, value_balance) -> list of (status, bvk bytes)"""
+        n = len(txs)
+        ns = (ctypes.c_uint32 * max(n, 1))(*[len(t[0]) for t in txs])
+        no = (ctypes.c_uint32 * max(n, 1))(*[len(t[1]) for t in txs])
+        vb = (ctypes.c_int64 * max(n, 1))(*[t[2] for t in txs])
+        cvs = b"".join(b"".join(map(bytes, t[0])) + b"".join(map(bytes, t[1])) for t in txs)
+        bvk = ctypes.create_string_buffer(max(32 * n, 1))
+        st = ctypes.create_string_buffer(max(n, 1))
+        self._chk(lib().zg_sapling_bvk(self._p, n, ns, no, cvs or None, vb, bvk, st))
+        return [(st.raw[i], bvk.raw[32 * i:32 * i + 32]) for i in range(n)]
+
+    def jubjub_decode(self, points):
+        """edwards::Point::read + small-order check -> list of (status 0/1/2, x, y ints)"""
+        n = len(points)
+        st = ctypes.create_string_buffer(max(n, 1))
+        xy = ctypes.create_string_buffer(max(64 * n, 1))
+        self._chk(lib().zg_jubjub_decode(self._p, n, b"".join(map(bytes, points)), st, xy))
+        return [(st.raw[i], int.from_bytes(xy.raw[64 * i:64 * i + 32], "little"),
+                 int.from_bytes(xy.raw[64 * i + 32:64 * i + 64], "little")) for i in range(n)]
 
     def chacha20_blocks(self, key, nonce, counter, nblocks):
         """the device ChaCha20 keystream (the batch-scalar CSPRNG), nblocks x 64 bytes"""
