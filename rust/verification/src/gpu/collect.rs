@@ -14,6 +14,7 @@
 //! The checks that are not Groth16 are evaluated by the caller as today and handed in as
 //! outcomes; every Groth16 proof of the block goes through ONE GpuVerifier::verify call.
 use super::{prep_joinsplit, prep_output, prep_spend, GpuError, GpuVerifier, Item};
+use super::ffi::{ZG_GEN_BINDING, ZG_GEN_SPEND_AUTH};
 use super::{ZG_KIND_OUTPUT, ZG_KIND_SPEND, ZG_KIND_SPROUT, ZG_STATUS_OK};
 
 pub struct JoinSplit {
@@ -37,8 +38,10 @@ pub struct Spend {
     pub nullifier: [u8; 32],
     pub rk: [u8; 32],
     pub zkproof: [u8; 192],
-    /// the caller's RedJubjub spend_auth_sig verdict
+    /// the caller's RedJubjub spend_auth_sig verdict, used when spend_auth_sig is None
     pub sig_ok: bool,
+    /// the signature, verified on the GPU when the transaction carries its sighash
+    pub spend_auth_sig: Option<[u8; 64]>,
 }
 
 pub struct Output {
@@ -58,8 +61,14 @@ pub struct Tx {
     pub js_nullifier_error: Option<String>,
     pub spends: Vec<Spend>,
     pub outputs: Vec<Output>,
+    /// the caller's binding_sig verdict, used when binding_sig is None
     pub binding_ok: bool,
     pub sapling_nullifier_error: Option<String>,
+    /// the no-input ZIP-243 sighash (accept_transaction.rs:374-386): with it, the spend_auth and
+    /// binding signatures are verified on the GPU
+    pub sighash: Option<[u8; 32]>,
+    pub value_balance: i64,
+    pub binding_sig: Option<[u8; 64]>,
 }
 
 #[derive(Debug, Clone, PartialEq)]
@@ -115,7 +124,61 @@ fn queue(txs: &[Tx]) -> (Vec<Item>, Vec<(Vec<Plan>, Vec<Plan>, Vec<Plan>)>) {
     (items, plans)
 }
 
-fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8]) -> Option<TxError> {
+/// (per-tx spend_auth verdicts, per-tx binding verdict): the GPU's for transactions with a
+/// sighash (one zg_sapling_bvk + one zg_redjubjub_verify call for the window), else the caller's
+fn sig_verdicts(v: &GpuVerifier, txs: &[Tx]) -> Result<(Vec<Vec<bool>>, Vec<bool>), GpuError> {
+    let mut sp: Vec<Vec<bool>> = txs.iter().map(|t| t.spends.iter().map(|s| s.sig_ok).collect()).collect();
+    let mut bind: Vec<bool> = txs.iter().map(|t| t.binding_ok).collect();
+    let need: Vec<usize> =
+        (0..txs.len()).filter(|&i| txs[i].sighash.is_some() && (!txs[i].spends.is_empty() || !txs[i].outputs.is_empty())).collect();
+    if need.is_empty() {
+        return Ok((sp, bind));
+    }
+    let rows: Vec<(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)> = need
+        .iter()
+        .map(|&i| (txs[i].spends.iter().map(|s| s.cv).collect(), txs[i].outputs.iter().map(|o| o.cv).collect(),
+                   txs[i].value_balance))
+        .collect();
+    let bvks = v.sapling_bvk(&rows)?;
+    let mut items = Vec::new();
+    let mut at = Vec::new();
+    for (&i, (st, bvk)) in need.iter().zip(bvks.iter()) {
+        let tx = &txs[i];
+        let sh = tx.sighash.unwrap();
+        for (j, s) in tx.spends.iter().enumerate() {
+            if let Some(sig) = s.spend_auth_sig {
+                let mut m = [0u8; 64];
+                m[..32].copy_from_slice(&s.rk);
+                m[32..].copy_from_slice(&sh);
+                items.push((s.rk, sig, m, ZG_GEN_SPEND_AUTH));
+                at.push((i, Some(j)));
+            }
+        }
+        if let Some(sig) = tx.binding_sig {
+            if *st == 0 {
+                let mut m = [0u8; 64];
+                m[..32].copy_from_slice(bvk);
+                m[32..].copy_from_slice(&sh);
+                items.push((*bvk, sig, m, ZG_GEN_BINDING));
+                at.push((i, None));
+            } else {
+                bind[i] = false;  // a cv that does not decode / InvalidBalanceValue
+            }
+        }
+    }
+    if !items.is_empty() {
+        for ((i, j), ok) in at.into_iter().zip(v.redjubjub_verify(&items)?) {
+            match j {
+                Some(j) => sp[i][j] = ok,
+                None => bind[i] = ok,
+            }
+        }
+    }
+    Ok((sp, bind))
+}
+
+fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8], sp_ok: &[bool], bind_ok: bool)
+            -> Option<TxError> {
     let (js, sp, out) = plan;
     if let Some(e) = &tx.pre_error {
         return Some(TxError::Caller(e.clone()));
@@ -142,9 +205,9 @@ fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8]) ->
         }
     }
     if !tx.spends.is_empty() || !tx.outputs.is_empty() {
-        for (s, p) in tx.spends.iter().zip(sp) {
+        for (ok, p) in sp_ok.iter().zip(sp) {
             let bad = match p {
-                Plan::Proof(k) => !s.sig_ok || status[*k] != ZG_STATUS_OK,
+                Plan::Proof(k) => !*ok || status[*k] != ZG_STATUS_OK,
                 _ => true,
             };
             if bad {
@@ -160,7 +223,7 @@ fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8]) ->
                 return Some(TxError::InvalidSapling);
             }
         }
-        if !tx.binding_ok {
+        if !bind_ok {
             return Some(TxError::InvalidSapling);
         }
         if let Some(e) = &tx.sapling_nullifier_error {
@@ -177,8 +240,9 @@ fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8]) ->
 pub fn verify_block(v: &GpuVerifier, txs: &[Tx]) -> Result<Option<(usize, TxError)>, GpuError> {
     let (items, plans) = queue(txs);
     let status = if items.is_empty() { Vec::new() } else { v.verify(&items)? };
+    let (sp_ok, bind_ok) = sig_verdicts(v, txs)?;
     for (idx, (tx, plan)) in txs.iter().zip(&plans).enumerate() {
-        if let Some(e) = tx_error(tx, plan, &status) {
+        if let Some(e) = tx_error(tx, plan, &status, &sp_ok[idx], bind_ok[idx]) {
             return Ok(Some((idx, e)));
         }
     }

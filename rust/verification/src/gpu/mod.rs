@@ -143,6 +143,53 @@ impl GpuVerifier {
     }
 }
 
+impl GpuVerifier {
+    /// RedJubjub PublicKey::read(vk) + verify(msg, sig, generator) for every item, on the GPU
+    /// (spend_auth_sig: vk = rk, msg = rk || sighash, ZG_GEN_SPEND_AUTH; binding_sig: vk = bvk,
+    /// msg = bvk || sighash, ZG_GEN_BINDING).
+    pub fn redjubjub_verify(&self, items: &[([u8; 32], [u8; 64], [u8; 64], u8)]) -> Result<Vec<bool>, GpuError> {
+        let _g = self.lock.lock().unwrap();
+        let n = items.len();
+        let mut vk = Vec::with_capacity(32 * n);
+        let mut sig = Vec::with_capacity(64 * n);
+        let mut msg = Vec::with_capacity(64 * n);
+        let mut gen = Vec::with_capacity(n);
+        for (v, s, m, g) in items {
+            vk.extend_from_slice(v);
+            sig.extend_from_slice(s);
+            msg.extend_from_slice(m);
+            gen.push(*g);
+        }
+        let mut ok = vec![0u8; n];
+        check(self.ctx, unsafe {
+            ffi::zg_redjubjub_verify(self.ctx, n, vk.as_ptr(), sig.as_ptr(), msg.as_ptr(), gen.as_ptr(), ok.as_mut_ptr())
+        })?;
+        Ok(ok.into_iter().map(|b| b == 1).collect())
+    }
+
+    /// binding verification keys: per tx (spend cvs, output cvs, valueBalance) -> (status, bvk)
+    pub fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError> {
+        let _g = self.lock.lock().unwrap();
+        let n = txs.len();
+        let ns: Vec<u32> = txs.iter().map(|t| t.0.len() as u32).collect();
+        let no: Vec<u32> = txs.iter().map(|t| t.1.len() as u32).collect();
+        let vb: Vec<i64> = txs.iter().map(|t| t.2).collect();
+        let mut cvs = Vec::new();
+        for t in txs {
+            for c in t.0.iter().chain(t.1.iter()) {
+                cvs.extend_from_slice(c);
+            }
+        }
+        let mut bvk = vec![0u8; 32 * n];
+        let mut st = vec![0u8; n];
+        check(self.ctx, unsafe {
+            ffi::zg_sapling_bvk(self.ctx, n, ns.as_ptr(), no.as_ptr(), cvs.as_ptr(), vb.as_ptr(), bvk.as_mut_ptr(),
+                                st.as_mut_ptr())
+        })?;
+        Ok((0..n).map(|i| (st[i], bvk[32 * i..32 * i + 32].try_into().unwrap())).collect())
+    }
+}
+
 impl Drop for GpuVerifier {
     fn drop(&mut self) {
         unsafe { ffi::zg_destroy(self.ctx) }

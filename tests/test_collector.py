@@ -178,3 +178,85 @@ def test_config5_replay_block_stream():
                 assert verify_block(txs, ctx=ctx) == (ti, ("InvalidJoinSplit", 0))
     finally:
         ctx.close()
+
+
+def signed_txs():
+    """the reference's real Sapling transactions with their sighash, signatures and valueBalance
+    (tests/golden/sapling_sigs.json): bd4fe81c (S1, O1), 991edf59 (S2, O3), 56afac11 (O2)"""
+    F = fields()
+    sg = load_golden("sapling_sigs.json")
+    sigs = {s["name"]: s for s in sg["sigs"]}
+    out = []
+    for t in sg["txs"]:
+        tx = make_tx(SRC_TX[t["name"]], F)
+        tx.sighash = h(t["sighash"])
+        tx.value_balance = t["value_balance"]
+        tx.binding_sig = h(t["binding_sig"])
+        for s in tx.spends:
+            s.spend_auth_sig = h(sigs[t["name"] + ":spend_auth"]["sig"])
+        out.append(tx)
+    return out
+
+
+def oracle_sig_fns():
+    from oracle import sapling_sig as S
+
+    def verify_sigs(vks, sigs, msgs, gens):
+        return [S.redjubjub_verify(v, s, m, g) for v, s, m, g in zip(vks, sigs, msgs, gens)]
+
+    def bvk(rows):
+        out = []
+        for sp, op, vb in rows:
+            try:
+                p = S.binding_verification_key(sp, op, vb)
+            except S.PointError:
+                out.append((1, bytes(32)))
+                continue
+            out.append((2, bytes(32)) if p is None else (0, S.encode(p)))
+        return out
+    return verify_sigs, bvk
+
+
+def _sig_cases(run):
+    txs = signed_txs()
+    assert run(txs) is None
+    txs = signed_txs()
+    assert [len(t.spends) for t in txs] == [1, 0, 1]
+    txs[2].spends[0].spend_auth_sig = bytes(64)            # BadSpendAuthSig -> InvalidSapling
+    assert run(txs) == (2, "InvalidSapling")
+    txs = signed_txs()
+    bs = bytearray(txs[1].binding_sig)
+    bs[40] ^= 1
+    txs[1].binding_sig = bytes(bs)                          # BadBindingSignature
+    assert run(txs) == (1, "InvalidSapling")
+    txs[0].spends[0].sig_ok = False                         # unchanged: the GPU verdict is used
+    assert run(txs) == (1, "InvalidSapling")
+    txs = signed_txs()
+    txs[0].value_balance = -(1 << 63)                       # InvalidBalanceValue
+    assert run(txs) == (0, "InvalidSapling")
+    txs = signed_txs()
+    txs[0].value_balance += 1                               # a different bvk: binding fails
+    assert run(txs) == (0, "InvalidSapling")
+    txs = signed_txs()
+    txs[0].sighash = None                                   # no sighash: the caller's verdicts
+    txs[0].binding_ok = False
+    assert run(txs) == (0, "InvalidSapling")
+
+
+def test_signatures_in_reference_order_cpu(cpu_verify):
+    """the window's RedJubjub checks (oracle verifier here) feed the same precedence"""
+    from zebra_amd.collector import verify_block
+    vs, bvk = oracle_sig_fns()
+    _sig_cases(lambda txs: verify_block(txs, verify=cpu_verify, verify_sigs=vs, sapling_bvk=bvk))
+
+
+@pytest.mark.gpu
+def test_signatures_in_reference_order_gpu():
+    """the same with every signature and binding key of the window on the GPU"""
+    from zebra_amd import Context
+    from zebra_amd.collector import verify_block
+    ctx = Context(device=0, max_batch=64)
+    try:
+        _sig_cases(lambda txs: verify_block(txs, ctx=ctx))
+    finally:
+        ctx.close()

@@ -54,7 +54,8 @@ class Spend:
     nullifier: bytes
     rk: bytes
     zkproof: bytes
-    sig_ok: bool = True               # caller's spend_auth_sig (RedJubjub) verdict
+    sig_ok: bool = True               # caller's spend_auth_sig (RedJubjub) verdict, used when
+    spend_auth_sig: Optional[bytes] = None   # ... this is None; else verified on the GPU
 
 
 @dataclass
@@ -75,8 +76,13 @@ class Tx:
     js_nullifier_error: Optional[str] = None
     spends: List[Spend] = field(default_factory=list)
     outputs: List[Output] = field(default_factory=list)
-    binding_ok: bool = True
+    binding_ok: bool = True                   # caller's binding_sig verdict, used when binding_sig is None
     sapling_nullifier_error: Optional[str] = None
+    # the Sapling signature checks on the GPU: the no-input ZIP-243 sighash the
+    # acceptor computes (accept_transaction.rs:374-386), valueBalance and the binding signature
+    sighash: Optional[bytes] = None
+    value_balance: int = 0
+    binding_sig: Optional[bytes] = None
 
 
 def _queue(txs):
@@ -113,9 +119,52 @@ def _queue(txs):
     return items, plans
 
 
-def _tx_error(tx, plan, status):
+def _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk):
+    """spend_auth_sig and binding_sig verdicts of the transactions that carry a sighash (the rest
+    keep the caller's booleans): the binding verification keys in one zg_sapling_bvk call, every
+    signature of the window in ONE zg_redjubjub_verify call (accept_spend sapling.rs:119-137,
+    accept_sapling_final :216-244). Returns (per-tx spend sig oks, per-tx binding ok)."""
+    if verify_sigs is None:
+        verify_sigs = ctx.redjubjub_verify if ctx is not None else None
+    if sapling_bvk is None:
+        sapling_bvk = ctx.sapling_bvk if ctx is not None else None
+    sp_ok = [[s.sig_ok for s in tx.spends] for tx in txs]
+    bind_ok = [tx.binding_ok for tx in txs]
+    need = [i for i, tx in enumerate(txs) if tx.sighash is not None and (tx.spends or tx.outputs)]
+    if not need:
+        return sp_ok, bind_ok
+    bvks = sapling_bvk([([s.cv for s in txs[i].spends], [o.cv for o in txs[i].outputs], txs[i].value_balance)
+                        for i in need])
+    items, where = [], []
+    for i, (st, bvk) in zip(need, bvks):
+        tx = txs[i]
+        for j, s in enumerate(tx.spends):
+            if s.spend_auth_sig is not None:
+                items.append((s.rk, s.spend_auth_sig, bytes(s.rk) + bytes(tx.sighash), zg.GEN_SPEND_AUTH))
+                where.append((i, j))
+        if tx.binding_sig is not None:
+            if st == 0:
+                items.append((bvk, tx.binding_sig, bvk + bytes(tx.sighash), zg.GEN_BINDING))
+                where.append((i, None))
+            else:   # a cv that does not decode fails its own description first; i64::MIN: InvalidBalanceValue
+                bind_ok[i] = False
+    if items:
+        oks = verify_sigs(*[list(x) for x in zip(*items)])
+        for (i, j), ok in zip(where, oks):
+            if j is None:
+                bind_ok[i] = ok
+            else:
+                sp_ok[i][j] = ok
+    return sp_ok, bind_ok
+
+
+def _tx_error(tx, plan, status, sp_ok=None, bind_ok=None):
     """the reference's first error of one transaction, given the proof statuses"""
     js_plan, sp_plan, out_plan = plan
+    if sp_ok is None:
+        sp_ok = [s.sig_ok for s in tx.spends]
+    if bind_ok is None:
+        bind_ok = tx.binding_ok
     if tx.pre_error:
         return tx.pre_error
     if tx.joinsplits:
@@ -130,13 +179,13 @@ def _tx_error(tx, plan, status):
         if tx.js_nullifier_error:
             return tx.js_nullifier_error
     if tx.spends or tx.outputs:
-        for s, (how, v) in zip(tx.spends, sp_plan):
-            if how == "prep" or not s.sig_ok or status[v] != OK:
+        for ok, (how, v) in zip(sp_ok, sp_plan):
+            if how == "prep" or not ok or status[v] != OK:
                 return "InvalidSapling"
         for how, v in out_plan:
             if how == "prep" or status[v] != OK:
                 return "InvalidSapling"
-        if not tx.binding_ok:
+        if not bind_ok:
             return "InvalidSapling"
         if tx.sapling_nullifier_error:
             return tx.sapling_nullifier_error
@@ -161,7 +210,7 @@ def _chunked(verify, cap):
     return run
 
 
-def verify_block(txs, verify=None, ctx=None):
+def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None):
     """Check the shielded proofs of a block (or an import window: a flat list of Tx in chain
     order). Returns None if every transaction passes, else (tx_index, error) with the error the
     reference reports (accept_chain.rs:79-80: the lowest failing index wins).
@@ -169,7 +218,8 @@ def verify_block(txs, verify=None, ctx=None):
     verify(proofs, kinds, inputs, n_inputs) -> statuses; default: ctx.verify_batch (ONE GPU
     batch for the whole block, exact per-proof statuses via bisection). A window larger than
     the context's max_batch (or a `verify.max_batch` attribute) is split into consecutive
-    batches."""
+    batches. Transactions that carry their sighash get their RedJubjub signatures verified on
+    the GPU too (verify_sigs / sapling_bvk default to ctx.redjubjub_verify / ctx.sapling_bvk)."""
     items, plans = _queue(txs)
     if verify is None:
         def verify(proofs, kinds, inputs, n_inputs):
@@ -185,8 +235,9 @@ def verify_block(txs, verify=None, ctx=None):
         inputs = zg.pack_inputs([inp for _, _, inp in items])
         n_inputs = bytes(len(inp) for _, _, inp in items)
         status = list(verify(proofs, kinds, inputs, n_inputs))
+    sp_ok, bind_ok = _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk)
     for idx, (tx, plan) in enumerate(zip(txs, plans)):
-        err = _tx_error(tx, plan, status)
+        err = _tx_error(tx, plan, status, sp_ok[idx], bind_ok[idx])
         if err is not None:
             return idx, err
     return None
