@@ -505,6 +505,62 @@ def gen_sapling_sigs():
     print("wrote sapling_sigs.json", len(txs), "txs", len(sigs), "sigs", len(sample), "sighash vectors")
 
 
+def gen_tree_state():
+    """tree_state.json: the note-commitment tree vectors of storage/src/tree_state.rs (the empty
+    roots of both trees and the expected roots of its tests), byte strings in storage order
+    (H256::from(hex) keeps the hex order, H256::from_reversed_str reverses it)"""
+    import re
+    src = open(os.path.join(REF, "storage/src/tree_state.rs")).read()
+    h256 = re.compile(r'H256::(from|from_reversed_str)\("([0-9a-f]{64})"\)')
+
+    def vals(text):
+        return [v if k == "from" else bytes.fromhex(v)[::-1].hex() for k, v in h256.findall(text)]
+
+    def block(start, end):
+        i = src.index(start)
+        return src[i:src.index(end, i + len(start))]
+
+    def test_body(name):
+        i = src.index("fn %s()" % name)
+        j = src.find("#[test]", i)
+        return src[i:j if j >= 0 else len(src)]
+
+    out = {"sprout_empty": vals(block("SPROUT_EMPTY_ROOTS: Vec<H256>", "].to_vec()")),
+           "sapling_empty": vals(block("SAPLING_EMPTY_ROOTS: Vec<H256>", "].to_vec()")),
+           "source": "storage/src/tree_state.rs (SPROUT_EMPTY_ROOTS, SAPLING_EMPTY_ROOTS and its tests)"}
+    commitments = vals(block("TEST_COMMITMENTS: Vec<H256>", "].to_vec()"))
+    cases = []
+    # (test, kind, height, leaves, roots after each append or one root at the end)
+    v = vals(test_body("single_root"))
+    cases.append({"test": "single_root", "kind": "sprout", "height": 1, "leaves": [out["sprout_empty"][0]],
+                  "final_root": v[-1]})
+    cases.append({"test": "empty_29_root", "kind": "sprout", "height": 29, "leaves": [],
+                  "final_root": vals(test_body("empty_29_root"))[0]})
+    v = vals(test_body("appended_1_29_root"))
+    cases.append({"test": "appended_1_29_root", "kind": "sprout", "height": 29, "leaves": v[:1], "final_root": v[1]})
+    v = vals(test_body("single_elem_in_double_tree"))
+    cases.append({"test": "single_elem_in_double_tree", "kind": "sprout", "height": 2,
+                  "leaves": [out["sprout_empty"][0]], "final_root": v[-1]})
+    v = vals(test_body("commitment_1"))
+    cases.append({"test": "commitment_1", "kind": "sprout", "height": 4, "leaves": v[:1], "final_root": v[1]})
+    v = vals(test_body("commitment_2"))
+    cases.append({"test": "commitment_2", "kind": "sprout", "height": 4, "leaves": v[:2], "final_root": v[2]})
+    v = vals(test_body("glass"))
+    cases.append({"test": "glass", "kind": "sprout", "height": 4, "leaves": commitments[:3], "final_root": v[6]})
+    roots = vals(test_body("commitments_full"))[:16]
+    cases.append({"test": "commitments_full", "kind": "sprout", "height": 4, "leaves": commitments,
+                  "roots": roots, "full_after": 16})
+    cases.append({"test": "sapling_empty_root", "kind": "sapling", "height": 32, "leaves": [],
+                  "final_root": vals(test_body("sapling_empty_root"))[0]})
+    v = vals(test_body("sapling_tree_state_root"))
+    cases.append({"test": "sapling_tree_state_root", "kind": "sapling", "height": 4, "leaves": v[:16],
+                  "roots": v[16:32]})
+    out["cases"] = cases
+    with open(os.path.join(HERE, "tree_state.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print("wrote tree_state.json", len(out["sprout_empty"]), len(out["sapling_empty"]), len(cases), "cases")
+
+
 def refresh_batch_gt():
     """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
     change of the batch-scalar mapping; no reference sources needed)"""
@@ -530,5 +586,7 @@ if __name__ == "__main__":
         gen_vk_codec()
     elif len(sys.argv) > 1 and sys.argv[1] == "--sapling-sigs":
         gen_sapling_sigs()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--tree-state":
+        gen_tree_state()
     else:
         main()
