@@ -65,6 +65,7 @@ extern "C" {
 #define ZG_E_VK (-4)      /* VK JSON/points failed to decode (crypto/src/json/groth16.rs:88-99) */
 #define ZG_E_NOMEM (-5)   /* batch larger than max_batch / allocation failure */
 #define ZG_E_STATE (-6)   /* batch API called out of order */
+#define ZG_E_TREE_FULL (-7) /* TreeState::append: "Appending to full tree" (tree_state.rs:238) */
 
 #define ZG_PROOF_BYTES 192
 #define ZG_FR_BYTES 32
@@ -193,6 +194,42 @@ int zg_redjubjub_verify(zg_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t*
 int zg_sapling_bvk(zg_ctx* ctx, size_t ntx, const uint32_t* n_spends, const uint32_t* n_outputs, const uint8_t* cvs,
                    const int64_t* value_balance, uint8_t* bvk, uint8_t* status);
 int zg_jubjub_decode(zg_ctx* ctx, size_t n, const uint8_t* points, uint8_t* status, uint8_t* xy);
+
+/* ---- note-commitment trees on the GPU. Hashes are H256 byte strings
+ * (32 B, storage order). kind ZG_TREE_SPROUT: SproutTreeHash, combine = sha256_compress
+ * (crypto/src/lib.rs:188-198); ZG_TREE_SAPLING: SaplingTreeHash, combine = pedersen_hash(left,
+ * right, depth) (crypto/src/lib.rs:250-275, Personalization::MerkleTree(depth), depth < 63).
+ *   zg_merkle_combine   <- TreeHash::combine (storage/src/tree_state.rs:175-177,188-190) on n
+ *        pairs: out[i] = combine(left[i], right[i], depth[i]) (depth NULL = all 0)
+ *   zg_tree_empty_roots <- H::empty() (tree_state.rs:5-138): levels (<= 64) entries, empty[0] =
+ *        the uncommitted leaf, empty[l + 1] = combine(empty[l], empty[l], l); computed on the
+ *        device on first use
+ *   zg_tree_roots       <- TreeState<D, H> (tree_state.rs:193-264) over a run of appends: from
+ *        `state` (the reference's serialized TreeState of this height, tree_state.rs:284-309;
+ *        NULL / state_len 0 = TreeState::new()) append the n_leaves leaves (n x 32 B) and write
+ *        roots[k] = root() after the first marks[k] of them (any order, each <= n_leaves):
+ *        one per block for the Sapling / Sprout block roots (db/src/block_chain_db.rs:254-304,
+ *        verification/src/accept_block.rs:290-320), one per JoinSplit for tree_cache.rs:57-71.
+ *        state_out (optional; capacity *state_out_len >= zg_tree_state_max_bytes(height)) gets
+ *        the serialized state after all n_leaves, *state_out_len its length. If the leaves
+ *        overflow the 2^height capacity: ZG_E_TREE_FULL, roots of the marks that fit are still
+ *        written (zeros for the others), state_out untouched. A state the appends could not
+ *        have produced (right or a parent without left, a parents list of another length) is
+ *        ZG_E_INVAL. Height 1..62 (29 Sprout H29, 32 Sapling H32).
+ *   zg_tree_roots_device: the same with the leaves already in device memory; kernel_ms
+ *        (optional) = device time of the level kernels (HIP events on the context stream) */
+#define ZG_TREE_SPROUT 0
+#define ZG_TREE_SAPLING 1
+int zg_merkle_combine(zg_ctx* ctx, int kind, size_t n, const uint8_t* left, const uint8_t* right,
+                      const uint8_t* depth, uint8_t* out);
+int zg_tree_empty_roots(zg_ctx* ctx, int kind, size_t levels, uint8_t* out);
+size_t zg_tree_state_max_bytes(int height);
+int zg_tree_roots(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len, size_t n_leaves,
+                  const uint8_t* leaves, size_t n_marks, const uint64_t* marks, uint8_t* roots, uint8_t* state_out,
+                  size_t* state_out_len);
+int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len,
+                         size_t n_leaves, const void* d_leaves, size_t n_marks, const uint64_t* marks,
+                         uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms);
 
 /* ---- synthetic workload (bench/tests): Groth16 re-randomization of real proofs,
  * out[i] = rerandomize(src[src_index[i]]) with (t, s) = BLAKE2b-512("zg-rerand"||seed||i)

@@ -240,16 +240,16 @@ class TreeState:
 
 
 def window_roots(state, leaves, marks):
-    """the roots after marks[k] of `leaves` are appended to `state` (marks nondecreasing), and
+    """the roots after marks[k] of `leaves` are appended to `state` (marks in any order), and
     the final state. A mark past the tree's capacity raises TreeFull after the roots before it
     were taken (the reference rejects that block: accept_block.rs:302-304)."""
     t = state.copy()
-    roots, done = [], 0
-    for m in marks:
-        while done < m:
+    roots, done = [None] * len(marks), 0
+    for k in sorted(range(len(marks)), key=lambda k: marks[k]):
+        while done < marks[k]:
             t.append(leaves[done])
             done += 1
-        roots.append(t.root())
+        roots[k] = t.root()
     while done < len(leaves):
         t.append(leaves[done])
         done += 1

@@ -39,6 +39,7 @@ pub const ZG_E_NOVK: c_int = -3;
 pub const ZG_E_VK: c_int = -4;
 pub const ZG_E_NOMEM: c_int = -5;
 pub const ZG_E_STATE: c_int = -6;
+pub const ZG_E_TREE_FULL: c_int = -7;
 
 pub const ZG_PROOF_BYTES: usize = 192;
 pub const ZG_FR_BYTES: usize = 32;
@@ -49,6 +50,8 @@ pub const ZG_R_BYTES: usize = 16;
 
 pub const ZG_GEN_SPEND_AUTH: u8 = 0;
 pub const ZG_GEN_BINDING: u8 = 1;
+pub const ZG_TREE_SPROUT: c_int = 0;
+pub const ZG_TREE_SAPLING: c_int = 1;
 
 pub const ZG_PREP_OK: c_int = 0;
 pub const ZG_PREP_VALUE_COMMITMENT_INVALID: c_int = 1;
@@ -103,6 +106,18 @@ extern "C" {
     pub fn zg_sapling_bvk(ctx: *mut ZgCtx, ntx: usize, n_spends: *const u32, n_outputs: *const u32, cvs: *const u8,
                           value_balance: *const i64, bvk: *mut u8, status: *mut u8) -> c_int;
     pub fn zg_jubjub_decode(ctx: *mut ZgCtx, n: usize, points: *const u8, status: *mut u8, xy: *mut u8) -> c_int;
+
+    pub fn zg_merkle_combine(ctx: *mut ZgCtx, kind: c_int, n: usize, left: *const u8, right: *const u8,
+                             depth: *const u8, out: *mut u8) -> c_int;
+    pub fn zg_tree_empty_roots(ctx: *mut ZgCtx, kind: c_int, levels: usize, out: *mut u8) -> c_int;
+    pub fn zg_tree_state_max_bytes(height: c_int) -> usize;
+    pub fn zg_tree_roots(ctx: *mut ZgCtx, kind: c_int, height: c_int, state: *const u8, state_len: usize,
+                         n_leaves: usize, leaves: *const u8, n_marks: usize, marks: *const u64, roots: *mut u8,
+                         state_out: *mut u8, state_out_len: *mut usize) -> c_int;
+    pub fn zg_tree_roots_device(ctx: *mut ZgCtx, kind: c_int, height: c_int, state: *const u8, state_len: usize,
+                                n_leaves: usize, d_leaves: *const c_void, n_marks: usize, marks: *const u64,
+                                roots: *mut u8, state_out: *mut u8, state_out_len: *mut usize,
+                                kernel_ms: *mut f32) -> c_int;
 
     pub fn zg_synth_rerandomize(ctx: *mut ZgCtx, n_src: usize, src_proofs: *const u8, src_kinds: *const u8,
                                 n: usize, src_index: *const u32, seed: u64, out_proofs: *mut u8) -> c_int;

@@ -31,6 +31,20 @@ using namespace zg;
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
 
+namespace zg {  // zg_merkle.hip
+struct MerkleDev;
+MerkleDev* merkle_dev_new();
+void merkle_dev_free(MerkleDev* m);
+int merkle_combine(MerkleDev* m, hipStream_t st, int kind, size_t n, const uint8_t* l, const uint8_t* r,
+                   const uint8_t* depth, uint8_t* out, std::string* err);
+int merkle_empty_roots(MerkleDev* m, hipStream_t st, int kind, size_t levels, uint8_t* out, std::string* err);
+size_t merkle_state_max_bytes(int height);
+int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const uint8_t* state, size_t state_len,
+                      size_t n, const void* leaves, int leaves_on_device, size_t nmarks, const uint64_t* marks,
+                      uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms,
+                      std::string* err);
+}  // namespace zg
+
 // Per-device state shared by every context (batch slot) on that GPU: a FIXED pool of stream
 // pairs, created once, and the prepared verifying keys. A context only owns buffers, so a
 // process can hold any number of slots without creating another HIP stream / hardware queue.
@@ -56,6 +70,7 @@ struct zg_dev {
   };
   std::vector<VKEntry*> vks;  // prepare_verifying_key once per distinct key per device
   uint32_t* jj_comb = nullptr;  // Jubjub generators' comb tables (zg_jubjub.h), built on first use
+  zg::MerkleDev* merkle = nullptr;  // Pedersen table + empty roots (zg_merkle.hip), first use
 };
 
 static std::mutex g_devs_mu;
@@ -156,6 +171,7 @@ static void dev_release(zg_dev* d) {
     delete e;
   }
   if (d->jj_comb) hipFree(d->jj_comb);
+  merkle_dev_free(d->merkle);
   g_devs[d->device] = nullptr;
   delete d;
 }
@@ -1332,4 +1348,62 @@ extern "C" int zg_chacha20_blocks(zg_ctx* ctx, const uint8_t key[32], const uint
   hipFree(d);
   if (e != hipSuccess) return fail(ctx, ZG_E_HIP, std::string("zg_chacha20_blocks: ") + hipGetErrorString(e));
   return ZG_OK;
+}
+
+// ------------------------------------------------------------------ note-commitment trees (zg_merkle.hip)
+static zg::MerkleDev* merkle_dev(zg_ctx* ctx) {
+  zg_dev* d = ctx->dev;
+  std::lock_guard<std::mutex> g(d->mu);
+  if (!d->merkle) d->merkle = merkle_dev_new();
+  return d->merkle;
+}
+
+extern "C" int zg_merkle_combine(zg_ctx* ctx, int kind, size_t n, const uint8_t* left, const uint8_t* right,
+                                 const uint8_t* depth, uint8_t* out) {
+  if (!ctx || (kind != ZG_TREE_SPROUT && kind != ZG_TREE_SAPLING) || (n && (!left || !right || !out)) ||
+      n > (1u << 30))
+    return ZG_E_INVAL;
+  if (kind == ZG_TREE_SAPLING && depth)
+    for (size_t i = 0; i < n; i++)
+      if (depth[i] >= 63) return fail(ctx, ZG_E_INVAL, "MerkleTree depth must be < 63");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return merkle_combine(merkle_dev(ctx), ctx->stream, kind, n, left, right, depth, out, &ctx->err);
+}
+
+extern "C" int zg_tree_empty_roots(zg_ctx* ctx, int kind, size_t levels, uint8_t* out) {
+  if (!ctx || (kind != ZG_TREE_SPROUT && kind != ZG_TREE_SAPLING) || levels > 64 || (levels && !out))
+    return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return merkle_empty_roots(merkle_dev(ctx), ctx->stream, kind, levels, out, &ctx->err);
+}
+
+extern "C" size_t zg_tree_state_max_bytes(int height) { return merkle_state_max_bytes(height); }
+
+static int tree_roots(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len, size_t n,
+                      const void* leaves, int on_device, size_t n_marks, const uint64_t* marks, uint8_t* roots,
+                      uint8_t* state_out, size_t* state_out_len, float* kernel_ms) {
+  if (!ctx || (kind != ZG_TREE_SPROUT && kind != ZG_TREE_SAPLING) || height < 1 || height > 62 ||
+      (n && !leaves) || (n_marks && (!marks || !roots)) || (state_len && !state) || n > (1ull << 40) ||
+      n_marks > (1u << 30))
+    return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return merkle_tree_roots(merkle_dev(ctx), ctx->stream, kind, height, state, state_len, n, leaves, on_device,
+                           n_marks, marks, roots, state_out, state_out_len, kernel_ms, &ctx->err);
+}
+
+extern "C" int zg_tree_roots(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len,
+                             size_t n_leaves, const uint8_t* leaves, size_t n_marks, const uint64_t* marks,
+                             uint8_t* roots, uint8_t* state_out, size_t* state_out_len) {
+  return tree_roots(ctx, kind, height, state, state_len, n_leaves, leaves, 0, n_marks, marks, roots, state_out,
+                    state_out_len, nullptr);
+}
+
+extern "C" int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len,
+                                    size_t n_leaves, const void* d_leaves, size_t n_marks, const uint64_t* marks,
+                                    uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms) {
+  return tree_roots(ctx, kind, height, state, state_len, n_leaves, d_leaves, 1, n_marks, marks, roots, state_out,
+                    state_out_len, kernel_ms);
 }

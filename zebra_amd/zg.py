@@ -10,6 +10,9 @@ LIB_PATH = os.path.join(HERE, "libzg.so")
 
 KIND_SPEND, KIND_OUTPUT, KIND_SPROUT = 0, 1, 2
 GEN_SPEND_AUTH, GEN_BINDING = 0, 1   # include/zg.h ZG_GEN_*
+TREE_SPROUT, TREE_SAPLING = 0, 1     # include/zg.h ZG_TREE_*
+SPROUT_HEIGHT, SAPLING_HEIGHT = 29, 32   # storage/src/tree_state.rs H29 / H32
+E_TREE_FULL = -7
 KIND_NINPUTS = {KIND_SPEND: 7, KIND_OUTPUT: 5, KIND_SPROUT: 9}
 STATUS_OK, STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "DECODE_INVALID", 2: "MALFORMED_VK", 3: "VERIFY_FAILED", 4: "INPUT_NONCANONICAL"}
@@ -67,6 +70,14 @@ def lib():
         L.zg_sapling_bvk.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), u8p,
                                      ctypes.POINTER(ctypes.c_int64), u8p, u8p]
         L.zg_jubjub_decode.argtypes = [vp, sz, u8p, u8p, u8p]
+        L.zg_merkle_combine.argtypes = [vp, i, sz, u8p, u8p, u8p, u8p]
+        L.zg_tree_empty_roots.argtypes = [vp, i, sz, u8p]
+        L.zg_tree_state_max_bytes.restype = sz
+        L.zg_tree_state_max_bytes.argtypes = [i]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.zg_tree_roots.argtypes = [vp, i, i, u8p, sz, sz, u8p, sz, u64p, u8p, u8p, ctypes.POINTER(sz)]
+        L.zg_tree_roots_device.argtypes = [vp, i, i, u8p, sz, sz, vp, sz, u64p, u8p, u8p, ctypes.POINTER(sz),
+                                           ctypes.POINTER(ctypes.c_float)]
         L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
         L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
         L.zg_prep_joinsplit.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
@@ -297,6 +308,54 @@ class Context:
         self._chk(lib().zg_jubjub_decode(self._p, n, b"".join(map(bytes, points)), st, xy))
         return [(st.raw[i], int.from_bytes(xy.raw[64 * i:64 * i + 32], "little"),
                  int.from_bytes(xy.raw[64 * i + 32:64 * i + 64], "little")) for i in range(n)]
+
+    # ---- note-commitment trees (include/zg.h zg_merkle_combine / zg_tree_*)
+    def merkle_combine(self, kind, lefts, rights, depths=None):
+        """TreeHash::combine on the GPU: [combine(l, r, depth)] as 32-byte strings"""
+        n = len(lefts)
+        assert len(rights) == n and (depths is None or len(depths) == n)
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        d = None if depths is None else bytes(depths)
+        self._chk(lib().zg_merkle_combine(self._p, kind, n, b"".join(map(bytes, lefts)),
+                                          b"".join(map(bytes, rights)), d, out))
+        return [out.raw[32 * j:32 * j + 32] for j in range(n)]
+
+    def tree_empty_roots(self, kind, levels=64):
+        """H::empty()[0..levels)"""
+        out = ctypes.create_string_buffer(32 * levels)
+        self._chk(lib().zg_tree_empty_roots(self._p, kind, levels, out))
+        return [out.raw[32 * j:32 * j + 32] for j in range(levels)]
+
+    def tree_roots(self, kind, height, state, leaves, marks, want_state=True, device_leaves=None,
+                   with_time=False):
+        """(roots after each marks[k] appended leaves, serialized final state or None).
+        state: the reference's serialized TreeState (b"" = new tree). device_leaves: a device
+        pointer holding the leaves (len(leaves) is then the count, an int). Raises ZgError
+        with code E_TREE_FULL past the capacity (the partial roots are on the exception)."""
+        state = bytes(state or b"")
+        nm = len(marks)
+        mk = (ctypes.c_uint64 * max(nm, 1))(*marks)
+        roots = ctypes.create_string_buffer(max(32 * nm, 1))
+        cap = lib().zg_tree_state_max_bytes(height)
+        so = ctypes.create_string_buffer(cap) if want_state else None
+        slen = ctypes.c_size_t(cap)
+        ms = ctypes.c_float(0)
+        if device_leaves is None:
+            n = len(leaves)
+            rc = lib().zg_tree_roots(self._p, kind, height, state, len(state), n, b"".join(map(bytes, leaves)),
+                                     nm, mk, roots, so, ctypes.byref(slen))
+        else:
+            n = int(leaves)
+            rc = lib().zg_tree_roots_device(self._p, kind, height, state, len(state), n,
+                                            ctypes.c_void_p(device_leaves), nm, mk, roots, so,
+                                            ctypes.byref(slen), ctypes.byref(ms))
+        rl = [roots.raw[32 * j:32 * j + 32] for j in range(nm)]
+        if rc:
+            e = ZgError(rc, lib().zg_last_error(self._p).decode(errors="replace"))
+            e.roots = rl
+            raise e
+        st = so.raw[:slen.value] if want_state else None
+        return (rl, st, ms.value) if with_time else (rl, st)
 
     def chacha20_blocks(self, key, nonce, counter, nblocks):
         """the device ChaCha20 keystream (the batch-scalar CSPRNG), nblocks x 64 bytes"""
