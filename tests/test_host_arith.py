@@ -40,6 +40,25 @@ def test_fq_ops(L):
             assert pow(int.from_bytes(out.raw, "big"), 2, P) == a
 
 
+def test_binary_gcd_inverse(L):
+    """zg_bingcd.h (Pornin's binary GCD, variable time) against pow(y, -1, p): Fr and Fq, random
+    and edge residues (0 -> 0, 1, p - 1, powers of two, values with long runs of equal bits)"""
+    rng = random.Random(4)
+    R = B.R
+    out = hostlib.buf(48)
+    edge_r = [0, 1, 2, R - 1, R - 2, 1 << 254, (1 << 255) % R, (1 << 200) - 1, R >> 1, 3]
+    for y in edge_r + [rng.randrange(R) for _ in range(3000)]:
+        L.zgt_fr_inv_vt(y.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw[:32], "little") == (pow(y, -1, R) if y else 0), hex(y)
+    for y in edge_r[:4] + [rng.randrange(1, R) for _ in range(300)]:
+        L.zgt_fr_inv_vt_mont(y.to_bytes(32, "little"), out)
+        assert int.from_bytes(out.raw[:32], "little") == (pow(y, -1, R) if y else 0), hex(y)
+    edge_q = [0, 1, 2, P - 1, P - 2, 1 << 380, (1 << 381) % P, (1 << 300) - 1, P >> 1]
+    for y in edge_q + [rng.randrange(P) for _ in range(1500)]:
+        L.zgt_fq_inv_vt(fq_b(y), out)
+        assert int.from_bytes(out.raw, "big") == (pow(y, -1, P) if y else 0), hex(y)
+
+
 def test_fr_mul(L):
     rng = random.Random(2)
     out = hostlib.buf(32)

@@ -31,7 +31,7 @@ def column(prods, tag):
     n = len(prods)
     for k, (x, y) in enumerate(prods):
         c = "%[c0]" if k % 2 == 0 else "%[c1]"
-        text.append("v_mad_u64_u32 %%[lm], %s, %s, %s, %%[lm]" % (c, op(x, "v"), op(y, "s" if y.startswith("FQ_P") else "v")))
+        text.append("v_mad_u64_u32 %%[lm], %s, %s, %s, %%[lm]" % (c, op(x, "v"), op(y, "s" if y.startswith(("FQ_P", "FR_R")) else "v")))
         if k >= 1:
             cp = "%[c0]" if (k - 1) % 2 == 0 else "%[c1]"
             text.append("v_addc_co_u32 %%[h], vcc, 0, %%[h], %s" % cp)
@@ -183,32 +183,41 @@ FQ_FNS = [("fqa_add", ["add"]), ("fqa_sub", ["sub"]), ("fqa_lzadd", ["lzadd"]), 
           ("f2a_lzsub", ["lzsub", "lzsub"]), ("f2a_sub_add", ["sub", "add"]), ("f2a_lzadd_lzsub", ["lzadd", "lzsub"])]
 
 
-def main():
-    out = ["// GENERATED by zebra_amd/csrc/gen_fips.py -- do not edit.", "#pragma once",
-           "// r = a * b * 2^-384 mod p ; a * b < 2^384 p (e.g. a < 4p, b < 2p)  ->  r < p",
-           "__device__ __forceinline__ void fq_mul_fips(uint32_t* r, const uint32_t* a, const uint32_t* b) {",
-           "  uint32_t m[12], t[12];", "  uint64_t lm = 0, c0, c1;", "  uint32_t h = 0;"]
-    for i in range(N):
+def gen_mul(name, n, pname, inv, rinv, bound, tbound):
+    """the FIPS Montgomery product over n limbs (modulus pname, -p^-1 mod 2^32 = inv)"""
+    out = ["// r = a * b * %s mod p ; a * b < 2^%d p (e.g. %s)  ->  r < p" % (rinv, 32 * n, bound),
+           "__device__ __forceinline__ void %s(uint32_t* r, const uint32_t* a, const uint32_t* b) {" % name,
+           "  uint32_t m[%d], t[%d];" % (n, n), "  uint64_t lm = 0, c0, c1;", "  uint32_t h = 0;"]
+    for i in range(n):
         prods = [("a[%d]" % j, "b[%d]" % (i - j)) for j in range(i + 1)]
-        prods += [("m[%d]" % j, "FQ_P[%d]" % (i - j)) for j in range(i)]
+        prods += [("m[%d]" % j, "%s[%d]" % (pname, i - j)) for j in range(i)]
         out.append(column(prods, "column %d: a b and m p products" % i))
-        out.append("  m[%d] = (uint32_t)lm * FQ_INV;" % i)
-        out.append(column([("m[%d]" % i, "FQ_P[0]")], "column %d: m_%d p_0" % (i, i)))
+        out.append("  m[%d] = (uint32_t)lm * %s;" % (i, inv))
+        out.append(column([("m[%d]" % i, "%s[0]" % pname)], "column %d: m_%d p_0" % (i, i)))
         out.append("  lm = (lm >> 32) | ((uint64_t)h << 32);")
         out.append("  h = 0;")
-    for i in range(N, 2 * N - 1):
-        prods = [("a[%d]" % j, "b[%d]" % (i - j)) for j in range(i - N + 1, N)]
-        prods += [("m[%d]" % j, "FQ_P[%d]" % (i - j)) for j in range(i - N + 1, N)]
+    for i in range(n, 2 * n - 1):
+        prods = [("a[%d]" % j, "b[%d]" % (i - j)) for j in range(i - n + 1, n)]
+        prods += [("m[%d]" % j, "%s[%d]" % (pname, i - j)) for j in range(i - n + 1, n)]
         out.append(column(prods, "column %d" % i))
-        out.append("  t[%d] = (uint32_t)lm;" % (i - N))
+        out.append("  t[%d] = (uint32_t)lm;" % (i - n))
         out.append("  lm = (lm >> 32) | ((uint64_t)h << 32);")
         out.append("  h = 0;")
-    out.append("  t[11] = (uint32_t)lm;  // < 2p < 2^382: no further carry")
-    out.append("  uint32_t pm[12];")
+    out.append("  t[%d] = (uint32_t)lm;  // %s: no further carry" % (n - 1, tbound))
+    out.append("  uint32_t pm[%d];" % n)
     out.append("#pragma unroll")
-    out.append("  for (int i = 0; i < 12; i++) pm[i] = FQ_P[i];")
-    out.append("  mp_reduce_once<12>(r, t, pm);")
+    out.append("  for (int i = 0; i < %d; i++) pm[i] = %s[i];" % (n, pname))
+    out.append("  mp_reduce_once<%d>(r, t, pm);" % n)
     out.append("}")
+    return out
+
+
+def main():
+    out = ["// GENERATED by zebra_amd/csrc/gen_fips.py -- do not edit.", "#pragma once"]
+    out += gen_mul("fq_mul_fips", 12, "FQ_P", "FQ_INV", "2^-384", "a < 4p, b < 2p", "< 2p < 2^382")
+    out.append("")
+    # Fr (the Jubjub base field): a, b < r < 2^255, so a b < 2^256 r and t < 2r < 2^256
+    out += gen_mul("fr_mul_fips", 8, "FR_R", "FR_INV", "2^-256", "a, b < r", "< 2r < 2^256")
     out.append("")
     # ---- lazy-reduction building blocks: the 24-limb product and the Montgomery reduction of a
     # 24-limb value, the same column statements split in two (an Fq2 Karatsuba product reduces

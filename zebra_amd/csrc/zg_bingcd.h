@@ -1,0 +1,224 @@
+// zg_bingcd.h -- variable-time modular inversion by binary GCD with 64-bit approximations
+// (T. Pornin, "Optimized Binary GCD for Modular Inversion", 2020, algorithm 2, k = 31).
+//
+// For PUBLIC values only (tree hashes, decoded points): the running time depends on the input.
+// It replaces Fermat's a^(p-2) (log2 p squarings + multiplications, ~380 Fr products) where an
+// inversion sits on a latency-critical chain: 17 outer steps (Fr) of 31 divsteps on 64-bit
+// approximations of a and b (their low 31 and top 33 bits), each followed by one linear update
+// of the full a, b (exact division by 2^31) and of the Bezout pair u, v (Montgomery division by
+// 2^31, so that a = y u and b = y v mod p hold throughout). 2 len(p) - 1 divsteps suffice for
+// b to reach gcd(y, p) = 1 (then v = y^-1); y = 0 returns 0, as a^(p-2) does.
+#pragma once
+#include "zg_field.h"
+
+namespace zg {
+
+// acc (N + 2 limbs, two's complement) += (neg ? -1 : 1) * a * m, a unsigned N limbs, m < 2^32
+template <int N>
+ZG_INL void bg_mac(uint32_t* acc, const uint32_t* a, uint32_t m, bool neg) {
+  const uint32_t mask = neg ? 0xffffffffu : 0u;
+  uint64_t c = 0, s = neg ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i < N + 2; i++) {
+    uint32_t p = 0;
+    if (i < N) {
+      c += (uint64_t)a[i] * m;
+      p = (uint32_t)c;
+      c >>= 32;
+    } else if (i == N) {
+      p = (uint32_t)c;
+    }
+    s += (uint64_t)acc[i] + (p ^ mask);
+    acc[i] = (uint32_t)s;
+    s >>= 32;
+  }
+}
+
+// t (N + 2 limbs, two's complement) >>= 31, arithmetic
+template <int N>
+ZG_INL void bg_shr31(uint32_t* t) {
+#pragma unroll
+  for (int i = 0; i < N + 1; i++) t[i] = (t[i] >> 31) | (t[i + 1] << 1);
+  t[N + 1] = (uint32_t)((int32_t)t[N + 1] >> 31);
+}
+
+template <int N>
+ZG_INL bool bg_neg_p(const uint32_t* t) {
+  return (int32_t)t[N + 1] < 0;
+}
+
+// t = -t when c (N + 2 limbs)
+template <int N>
+ZG_INL void bg_cneg(uint32_t* t, bool c) {
+  const uint32_t mask = c ? 0xffffffffu : 0u;
+  uint64_t s = c ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i < N + 2; i++) {
+    s += (uint64_t)(t[i] ^ mask);
+    t[i] = (uint32_t)s;
+    s >>= 32;
+  }
+}
+
+// t += c ? sign * p : 0 (N + 2 limbs)
+template <class M>
+ZG_INL void bg_cadd_p(uint32_t* t, bool c, bool sub) {
+  constexpr int N = M::N;
+  const uint32_t mask = sub ? 0xffffffffu : 0u;
+  uint64_t s = sub ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i < N + 2; i++) {
+    const uint32_t pi = c ? ((i < N ? M::p(i) : 0u) ^ mask) : 0u;
+    s += (uint64_t)t[i] + pi;
+    t[i] = (uint32_t)s;
+    s >>= 32;
+  }
+  (void)s;
+}
+
+// limb i of a (i may be anything in [0, N]; N gives 0): a select chain, no indexed registers
+template <int N>
+ZG_INL uint32_t bg_limb(const uint32_t* a, int i) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++) v = i == j ? a[j] : v;
+  return v;
+}
+
+template <int N>
+ZG_INL int bg_bitlen(const uint32_t* a) {
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < N; j++) n = a[j] ? 32 * j + 32 - __builtin_clz(a[j]) : n;
+  return n;
+}
+
+// 64 bits of a starting at bit `off` (0 <= off < 32 N)
+template <int N>
+ZG_INL uint64_t bg_bits64(const uint32_t* a, int off) {
+  const int w = off >> 5, sh = off & 31;
+  const uint64_t lo = bg_limb<N>(a, w), mid = bg_limb<N>(a, w + 1), hi = bg_limb<N>(a, w + 2);
+  const uint64_t x = lo | (mid << 32);
+  return sh ? (x >> sh) | (hi << (64 - sh)) : x;
+}
+
+// y^-1 mod p for a residue y in [0, p) (any representation: the caller fixes Montgomery factors)
+template <class M, int T>
+ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
+  constexpr int N = M::N;
+  uint32_t a[N], b[N], u[N], v[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    a[i] = y.l[i];
+    b[i] = M::p(i);
+    u[i] = i == 0 ? 1u : 0u;
+    v[i] = 0;
+  }
+  for (int it = 0; it < T; it++) {
+    int n = bg_bitlen<N>(a);
+    const int nb = bg_bitlen<N>(b);
+    n = n > nb ? n : nb;
+    n = n > 64 ? n : 64;
+    const uint64_t low = (1ull << 31) - 1;
+    uint64_t xa = ((uint64_t)a[0] & low) | ((bg_bits64<N>(a, n - 33) & ((1ull << 33) - 1)) << 31);
+    uint64_t xb = ((uint64_t)b[0] & low) | ((bg_bits64<N>(b, n - 33) & ((1ull << 33) - 1)) << 31);
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 4
+    for (int j = 0; j < 31; j++) {
+      const bool odd = xa & 1;
+      const bool sw = odd && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xa = (odd ? ta - tb : ta) >> 1;
+      xb = tb;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      f1 = tf1 << 1;
+      g1 = tg1 << 1;
+    }
+    // (a, b) <- ((a f0 + b g0) / 2^31, (a f1 + b g1) / 2^31), signs folded into the factors
+    uint32_t na[N + 2], nb2[N + 2];
+#pragma unroll
+    for (int i = 0; i < N + 2; i++) na[i] = nb2[i] = 0;
+    bg_mac<N>(na, a, (uint32_t)(f0 < 0 ? -f0 : f0), f0 < 0);
+    bg_mac<N>(na, b, (uint32_t)(g0 < 0 ? -g0 : g0), g0 < 0);
+    bg_mac<N>(nb2, a, (uint32_t)(f1 < 0 ? -f1 : f1), f1 < 0);
+    bg_mac<N>(nb2, b, (uint32_t)(g1 < 0 ? -g1 : g1), g1 < 0);
+    bg_shr31<N>(na);
+    bg_shr31<N>(nb2);
+    const bool fa = bg_neg_p<N>(na), fb = bg_neg_p<N>(nb2);
+    bg_cneg<N>(na, fa);
+    bg_cneg<N>(nb2, fb);
+    if (fa) {
+      f0 = -f0;
+      g0 = -g0;
+    }
+    if (fb) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      a[i] = na[i];
+      b[i] = nb2[i];
+    }
+    // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31) mod p (Montgomery division)
+    uint32_t nu[N + 2], nv[N + 2];
+#pragma unroll
+    for (int i = 0; i < N + 2; i++) nu[i] = nv[i] = 0;
+    bg_mac<N>(nu, u, (uint32_t)(f0 < 0 ? -f0 : f0), f0 < 0);
+    bg_mac<N>(nu, v, (uint32_t)(g0 < 0 ? -g0 : g0), g0 < 0);
+    bg_mac<N>(nv, u, (uint32_t)(f1 < 0 ? -f1 : f1), f1 < 0);
+    bg_mac<N>(nv, v, (uint32_t)(g1 < 0 ? -g1 : g1), g1 < 0);
+    uint32_t pm[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) pm[i] = M::p(i);
+    bg_mac<N>(nu, pm, (nu[0] * M::INV) & 0x7fffffffu, false);
+    bg_mac<N>(nv, pm, (nv[0] * M::INV) & 0x7fffffffu, false);
+    bg_shr31<N>(nu);
+    bg_shr31<N>(nv);
+    // now in (-3p, 3p): into [0, p)
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      bg_cadd_p<M>(nu, bg_neg_p<N>(nu), false);
+      bg_cadd_p<M>(nv, bg_neg_p<N>(nv), false);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      uint32_t tu[N + 2], tv[N + 2];
+#pragma unroll
+      for (int i = 0; i < N + 2; i++) {
+        tu[i] = nu[i];
+        tv[i] = nv[i];
+      }
+      bg_cadd_p<M>(tu, true, true);
+      bg_cadd_p<M>(tv, true, true);
+      const bool ku = !bg_neg_p<N>(tu), kv = !bg_neg_p<N>(tv);
+#pragma unroll
+      for (int i = 0; i < N + 2; i++) {
+        nu[i] = ku ? tu[i] : nu[i];
+        nv[i] = kv ? tv[i] : nv[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      u[i] = nu[i];
+      v[i] = nv[i];
+    }
+  }
+  // b == 1 unless y == 0 (then v == 0 too)
+  Fp<M> r;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.l[i] = v[i];
+  return r;
+}
+
+// Montgomery-form inverse of a Montgomery-form Fr (public values): (a R)^-1 R^3 R^-1 = a^-1 R
+ZG_INL Fr fr_inv_vt(const Fr& a) {
+  Fr r3;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r3.l[i] = FR_R3[i];
+  return fr_mul(fp_inv_vt<FrM, 17>(a), r3);
+}
+
+}  // namespace zg

@@ -268,7 +268,12 @@ ZG_NOINL inline u32x8 fr_mul_v(u32x8 a0, u32x8 b0) {
     a.l[i] = a0[i];
     b.l[i] = b0[i];
   }
-  Fr r = fp_mul_inl<FrM>(a, b);
+  Fr r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  fr_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning
+#else
+  r = fp_mul_inl<FrM>(a, b);   // host build of the test harness (tests/native): portable CIOS
+#endif
   u32x8 o;
 #pragma unroll
   for (int i = 0; i < 8; i++) o[i] = r.l[i];

@@ -20,6 +20,7 @@
 // the device by k_ph_table on first use.
 #pragma once
 #include "../../include/zg.h"  // ZG_TREE_SPROUT / ZG_TREE_SAPLING
+#include "zg_bingcd.h"
 #include "zg_jubjub.h"
 
 namespace zg {
@@ -31,14 +32,38 @@ namespace zg {
 #define ZG_PH_POINTS (ZG_PH_GENS * ZG_PH_WIN * ZG_PH_CODES)
 #define ZG_PH_TABLE_BYTES ((size_t)ZG_PH_POINTS * ZG_PH_WORDS * 4)
 
+// The Pedersen additions multiply with the inlined product-scanning Montgomery product
+// (fr_mul_fips, ~2 instructions per 32x32 MAC) rather than the out-of-line CIOS fr_mul: a hash
+// group is a lone wave on a latency-bound chain of tree levels, so its time is the number of
+// instructions it issues.
+ZG_INL Fr ph_mul(const Fr& a, const Fr& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  Fr r;
+  fr_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning (zg_fips.h)
+  return r;
+#else
+  return fp_mul_inl<FrM>(a, b);
+#endif
+}
+
 // add-2008-hwcd-3 (a = -1, k = 2d), q given as a niels point (affine): 7 multiplications
 ZG_INL JExt jx_add_niels(const JExt& p, const Fr& ypx, const Fr& ymx, const Fr& k) {
-  const Fr A = fr_mul(fp_sub<FrM>(p.Y, p.X), ymx);
-  const Fr B = fr_mul(fr_add(p.Y, p.X), ypx);
-  const Fr C = fr_mul(p.T, k);
+  const Fr A = ph_mul(fp_sub<FrM>(p.Y, p.X), ymx);
+  const Fr B = ph_mul(fr_add(p.Y, p.X), ypx);
+  const Fr C = ph_mul(p.T, k);
   const Fr D = fr_add(p.Z, p.Z);
   const Fr E = fp_sub<FrM>(B, A), F = fp_sub<FrM>(D, C), G = fr_add(D, C), H = fr_add(B, A);
-  return {fr_mul(E, F), fr_mul(G, H), fr_mul(F, G), fr_mul(E, H)};
+  return {ph_mul(E, F), ph_mul(G, H), ph_mul(F, G), ph_mul(E, H)};
+}
+// add-2008-hwcd (a = -1), both extended: 9 multiplications (d folded into 2d T2 / 2 = d T2)
+ZG_INL JExt ph_add(const JExt& p, const JExt& q) {
+  const Fr A = ph_mul(p.X, q.X);
+  const Fr B = ph_mul(p.Y, q.Y);
+  const Fr C = ph_mul(ph_mul(p.T, q.T), jj_const(JUBJUB_D));
+  const Fr D = ph_mul(p.Z, q.Z);
+  const Fr E = fp_sub<FrM>(fp_sub<FrM>(ph_mul(fr_add(p.X, p.Y), fr_add(q.X, q.Y)), A), B);
+  const Fr F = fp_sub<FrM>(D, C), G = fr_add(D, C), H = fr_add(B, A);
+  return {ph_mul(E, F), ph_mul(G, H), ph_mul(F, G), ph_mul(E, H)};
 }
 
 // enc(a, b, c) of a 3-bit chunk (a = bit 0): (1 - 2c)(1 + a + 2b)
@@ -68,33 +93,66 @@ ZG_INL void ph_stream(const uint32_t* lw, const uint32_t* rw, int depth, uint32_
   }
 }
 
-// Pedersen MerkleTree(depth) hash of two LE 256-bit words -> the canonical u coordinate
-ZG_INL void ph_merkle(const uint32_t* lw, const uint32_t* rw, int depth, const uint32_t* table, uint32_t* out) {
+// 17-way select: word k of the stream (k in [0, 17]; 17 gives 0) without indexed registers
+ZG_INL uint32_t ph_word(const uint32_t* s, int k) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 17; j++) v = k == j ? s[j] : v;
+  return v;
+}
+
+// Pedersen MerkleTree(depth) hash of two LE 256-bit words -> the canonical u coordinate, on a
+// group of LANES consecutive lanes (all active, `sub` = the lane's index in the group):
+// lane j adds the table points of windows j, j + 8, ... (11 of the 87), the 8 partial sums meet
+// in a 3-round xor butterfly (full additions), and every lane of the group then holds the sum;
+// the affine u = X / Z uses the binary-GCD inverse (public data). Only sub == 0 writes `out`.
+// A lone wave's Fr product costs ~1.1 us (its ~450 VALU instructions at 4 cycles each), so a
+// hash's latency is the instructions one lane runs: ceil(87 / LANES) niels additions plus
+// log2(LANES) butterfly additions plus the inversion (8 lanes: 11 + 3; 32 lanes: 3 + 5). Wide
+// groups shorten the latency-bound upper tree levels, narrow ones spend less on butterflies
+// where a level has enough hashes to fill the chip (zg_merkle.hip picks per launch).
+#define ZG_PH_LANES_NARROW 8
+#define ZG_PH_LANES_WIDE 32
+#define ZG_PH_WINDOWS 87
+template <int LANES>
+ZG_INL void ph_merkle(const uint32_t* lw, const uint32_t* rw, int depth, const uint32_t* table, int sub,
+                      uint32_t* out) {
   uint32_t s[17];
   ph_stream(lw, rw, depth, s);
   JExt acc = jx_zero();
-  for (int g = 0; g < ZG_PH_GENS; g++) {
-    const int npairs = g < 2 ? ZG_PH_WIN : 23;
-    for (int w = 0; w < npairs; w++) {
-      const bool single = w == ZG_PH_WIN - 1;  // chunk 62 of a full segment
-      const uint32_t code = s[0] & (single ? 7u : 63u);
-      const uint4* e = (const uint4*)(table + ((size_t)((g * ZG_PH_WIN + w) * ZG_PH_CODES) + code) * ZG_PH_WORDS);
-      Fr ypx, ymx, k;
-      const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4], e5 = e[5];
-      ypx.l[0] = e0.x, ypx.l[1] = e0.y, ypx.l[2] = e0.z, ypx.l[3] = e0.w;
-      ypx.l[4] = e1.x, ypx.l[5] = e1.y, ypx.l[6] = e1.z, ypx.l[7] = e1.w;
-      ymx.l[0] = e2.x, ymx.l[1] = e2.y, ymx.l[2] = e2.z, ymx.l[3] = e2.w;
-      ymx.l[4] = e3.x, ymx.l[5] = e3.y, ymx.l[6] = e3.z, ymx.l[7] = e3.w;
-      k.l[0] = e4.x, k.l[1] = e4.y, k.l[2] = e4.z, k.l[3] = e4.w;
-      k.l[4] = e5.x, k.l[5] = e5.y, k.l[6] = e5.z, k.l[7] = e5.w;
-      acc = jx_add_niels(acc, ypx, ymx, k);
-      const int sh = single ? 3 : 6;
-#pragma unroll
-      for (int i = 0; i < 16; i++) s[i] = (s[i] >> sh) | (s[i + 1] << (32 - sh));
-      s[16] >>= sh;
-    }
+  for (int w = sub; w < ZG_PH_WINDOWS; w += LANES) {
+    const int g = w >> 5, wi = w & 31;
+    const int pos = 3 * (63 * g + 2 * wi);  // the window's first stream bit
+    const int k = pos >> 5, sh = pos & 31;
+    const uint32_t lo = ph_word(s, k), hi = ph_word(s, k + 1);
+    const uint32_t code = ((lo >> sh) | (sh ? hi << (32 - sh) : 0u)) & (wi == ZG_PH_WIN - 1 ? 7u : 63u);
+    const uint4* e = (const uint4*)(table + ((size_t)((g * ZG_PH_WIN + wi) * ZG_PH_CODES) + code) * ZG_PH_WORDS);
+    Fr ypx, ymx, kk;
+    const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3], e4 = e[4], e5 = e[5];
+    ypx.l[0] = e0.x, ypx.l[1] = e0.y, ypx.l[2] = e0.z, ypx.l[3] = e0.w;
+    ypx.l[4] = e1.x, ypx.l[5] = e1.y, ypx.l[6] = e1.z, ypx.l[7] = e1.w;
+    ymx.l[0] = e2.x, ymx.l[1] = e2.y, ymx.l[2] = e2.z, ymx.l[3] = e2.w;
+    ymx.l[4] = e3.x, ymx.l[5] = e3.y, ymx.l[6] = e3.z, ymx.l[7] = e3.w;
+    kk.l[0] = e4.x, kk.l[1] = e4.y, kk.l[2] = e4.z, kk.l[3] = e4.w;
+    kk.l[4] = e5.x, kk.l[5] = e5.y, kk.l[6] = e5.z, kk.l[7] = e5.w;
+    acc = jx_add_niels(acc, ypx, ymx, kk);
   }
-  const Fr x = fr_from_mont(fr_mul(acc.X, prep_fr_inv(acc.Z)));
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+  for (int m = 1; m < LANES; m <<= 1) {
+    JExt o;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o.X.l[i] = (uint32_t)__shfl_xor((int)acc.X.l[i], m);
+      o.Y.l[i] = (uint32_t)__shfl_xor((int)acc.Y.l[i], m);
+      o.Z.l[i] = (uint32_t)__shfl_xor((int)acc.Z.l[i], m);
+      o.T.l[i] = (uint32_t)__shfl_xor((int)acc.T.l[i], m);
+    }
+    acc = ph_add(acc, o);
+  }
+#endif
+  if (sub) return;
+  const Fr x = fr_from_mont(fr_mul(acc.X, fr_inv_vt(acc.Z)));
 #pragma unroll
   for (int i = 0; i < 8; i++) out[i] = x.l[i];
 }
@@ -156,8 +214,10 @@ __device__ __forceinline__ void sha256_compress_words(const uint32_t* lw, const 
   out[7] = __builtin_bswap32(iv[7] + h);
 }
 
-template <int KIND>
-ZG_INL void tree_combine(const uint32_t* l, const uint32_t* r, int depth, const uint32_t* table, uint32_t* out) {
+// LANES lanes per hash: Pedersen on a group (8 or 32), SHA-256 on one lane (LANES = 1)
+template <int KIND, int LANES>
+ZG_INL void tree_combine(const uint32_t* l, const uint32_t* r, int depth, const uint32_t* table, int sub,
+                         uint32_t* out) {
   uint32_t lw[8], rw[8];
   const uint4* l4 = (const uint4*)l;
   const uint4* r4 = (const uint4*)r;
@@ -165,10 +225,12 @@ ZG_INL void tree_combine(const uint32_t* l, const uint32_t* r, int depth, const 
   lw[0] = a0.x, lw[1] = a0.y, lw[2] = a0.z, lw[3] = a0.w, lw[4] = a1.x, lw[5] = a1.y, lw[6] = a1.z, lw[7] = a1.w;
   rw[0] = b0.x, rw[1] = b0.y, rw[2] = b0.z, rw[3] = b0.w, rw[4] = b1.x, rw[5] = b1.y, rw[6] = b1.z, rw[7] = b1.w;
   uint32_t o[8];
-  if (KIND == ZG_TREE_SPROUT)
+  if (KIND == ZG_TREE_SPROUT) {
     sha256_compress_words(lw, rw, o);
-  else
-    ph_merkle(lw, rw, depth, table, o);
+  } else {
+    ph_merkle<LANES>(lw, rw, depth, table, sub, o);
+    if (sub) return;
+  }
   uint4* o4 = (uint4*)out;
   o4[0] = make_uint4(o[0], o[1], o[2], o[3]);
   o4[1] = make_uint4(o[4], o[5], o[6], o[7]);

@@ -59,29 +59,31 @@ __global__ void __launch_bounds__(64) k_ph_table(uint32_t* table) {
   }
 }
 
-template <int KIND>
+template <int KIND, int LANES>
 __global__ void __launch_bounds__(64) k_merkle_combine(int n, const uint32_t* l, const uint32_t* r,
                                                        const uint8_t* depth, const uint32_t* table, uint32_t* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long t = blockIdx.x * 64ll + threadIdx.x;
+  const int i = (int)(t / LANES), sub = (int)(t % LANES);
   if (i >= n) return;
-  tree_combine<KIND>(l + 8 * (size_t)i, r + 8 * (size_t)i, depth ? depth[i] : 0, table, out + 8 * (size_t)i);
+  tree_combine<KIND, LANES>(l + 8 * (size_t)i, r + 8 * (size_t)i, depth ? depth[i] : 0, table, sub, out + 8 * (size_t)i);
 }
 
 // H::empty() one level at a time: e[l + 1] = combine(e[l], e[l], l) (a one-time, per device
 // table; e[0], the uncommitted leaf, is written by the host)
-template <int KIND>
+template <int KIND, int LANES>
 __global__ void __launch_bounds__(64) k_tree_empty_step(uint32_t* e, int l, const uint32_t* table) {
-  if (blockIdx.x | threadIdx.x) return;
-  tree_combine<KIND>(e + 8 * l, e + 8 * l, l, table, e + 8 * (l + 1));
+  if (blockIdx.x || threadIdx.x >= LANES) return;
+  tree_combine<KIND, LANES>(e + 8 * l, e + 8 * l, l, table, threadIdx.x, e + 8 * (l + 1));
 }
 
 // one level: items [0, nm) advance a root walk (pos = leaf index of the root's last leaf),
 // items [nm, nm + cnt_next) build the next level's nodes base_next + j
-template <int KIND>
+template <int KIND, int LANES>
 __global__ void __launch_bounds__(64) k_tree_level(TreeLevel L, int level, int nm, const unsigned long long* pos,
                                                    uint32_t* cur, uint32_t* wnext, long long base_next,
                                                    long long cnt_next, const uint32_t* table) {
-  const long long t = blockIdx.x * 64ll + threadIdx.x;
+  const long long t = (blockIdx.x * 64ll + threadIdx.x) / LANES;
+  const int sub = (int)(threadIdx.x % LANES);
   const uint32_t *a, *b;
   uint32_t* o;
   if (t < nm) {
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(64) k_tree_level(TreeLevel L, int level, int n
   } else {
     return;
   }
-  tree_combine<KIND>(a, b, level, table, o);
+  tree_combine<KIND, LANES>(a, b, level, table, sub, o);
 }
 
 __global__ void k_gather32(int n, const uint32_t* const* src, uint32_t* out) {
@@ -177,9 +179,9 @@ static int merkle_ready(MerkleDev* m, hipStream_t st, int kind, std::string* err
     hipError_t he = hipMemcpyAsync(e, e0, 32, hipMemcpyHostToDevice, st);
     for (int l = 0; he == hipSuccess && l + 1 < ZG_TREE_EMPTY_LEVELS; l++) {
       if (kind == ZG_TREE_SAPLING)
-        hipLaunchKernelGGL(k_tree_empty_step<ZG_TREE_SAPLING>, dim3(1), dim3(64), 0, st, e, l, (const uint32_t*)m->ph);
+        hipLaunchKernelGGL((k_tree_empty_step<ZG_TREE_SAPLING, ZG_PH_LANES_WIDE>), dim3(1), dim3(64), 0, st, e, l, (const uint32_t*)m->ph);
       else
-        hipLaunchKernelGGL(k_tree_empty_step<ZG_TREE_SPROUT>, dim3(1), dim3(64), 0, st, e, l, (const uint32_t*)m->ph);
+        hipLaunchKernelGGL((k_tree_empty_step<ZG_TREE_SPROUT, 1>), dim3(1), dim3(64), 0, st, e, l, (const uint32_t*)m->ph);
       he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipMemcpyAsync(m->empty_h[kind], e, ZG_TREE_EMPTY_LEVELS * 32, hipMemcpyDeviceToHost, st);
@@ -211,10 +213,10 @@ int merkle_combine(MerkleDev* m, hipStream_t st, int kind, size_t n, const uint8
     MCHK(hipMemcpyAsync(dd, depth, n, hipMemcpyHostToDevice, st));
   }
   if (kind == ZG_TREE_SAPLING)
-    hipLaunchKernelGGL(k_merkle_combine<ZG_TREE_SAPLING>, dim3(blocks64(n)), dim3(64), 0, st, (int)n, dl, dr, dd,
-                       (const uint32_t*)m->ph, dout);
+    hipLaunchKernelGGL((k_merkle_combine<ZG_TREE_SAPLING, ZG_PH_LANES_NARROW>), dim3(blocks64(n * ZG_PH_LANES_NARROW)),
+                       dim3(64), 0, st, (int)n, dl, dr, dd, (const uint32_t*)m->ph, dout);
   else
-    hipLaunchKernelGGL(k_merkle_combine<ZG_TREE_SPROUT>, dim3(blocks64(n)), dim3(64), 0, st, (int)n, dl, dr, dd,
+    hipLaunchKernelGGL((k_merkle_combine<ZG_TREE_SPROUT, 1>), dim3(blocks64(n)), dim3(64), 0, st, (int)n, dl, dr, dd,
                        (const uint32_t*)m->ph, dout);
   MCHK(hipGetLastError());
   MCHK(hipMemcpyAsync(out, dout, 32 * n, hipMemcpyDeviceToHost, st));
@@ -283,12 +285,15 @@ static size_t write_state(const HostTree& t, uint8_t* out) {
 
 size_t merkle_state_max_bytes(int height) { return 2 * 33 + 1 + (size_t)(height > 0 ? height - 1 : 0) * 33; }
 
-template <int KIND>
+// Sapling levels with at most ZG_PH_WIDE_ITEMS hashes (one 32-lane group per SIMD, about) run
+// wide groups: their time is one hash's latency. Bigger levels run 8-lane groups.
+#define ZG_PH_WIDE_ITEMS 512
+template <int KIND, int LANES>
 static void launch_level(hipStream_t st, const TreeLevel& L, int level, int nm, const unsigned long long* pos,
                          uint32_t* cur, uint32_t* wnext, long long base_next, long long cnt_next,
                          const uint32_t* table) {
-  hipLaunchKernelGGL(k_tree_level<KIND>, dim3(blocks64(nm + cnt_next)), dim3(64), 0, st, L, level, nm, pos, cur,
-                     wnext, base_next, cnt_next, table);
+  hipLaunchKernelGGL((k_tree_level<KIND, LANES>), dim3(blocks64((nm + cnt_next) * LANES)), dim3(64), 0, st, L,
+                     level, nm, pos, cur, wnext, base_next, cnt_next, table);
 }
 
 int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const uint8_t* state, size_t state_len,
@@ -393,12 +398,14 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
     const bool top = l + 1 == height;
     const long long cnt_next = top ? 0 : L[l + 1].cnt;
     if (!nm && !cnt_next) continue;
-    if (kind == ZG_TREE_SAPLING)
-      launch_level<ZG_TREE_SAPLING>(st, L[l], l, nm, dpos, dcur, top ? nullptr : wbuf[l + 1],
-                                    top ? 0 : L[l + 1].base, cnt_next, m->ph);
+    uint32_t* wn = top ? nullptr : wbuf[l + 1];
+    const long long bn = top ? 0 : L[l + 1].base;
+    if (kind == ZG_TREE_SPROUT)
+      launch_level<ZG_TREE_SPROUT, 1>(st, L[l], l, nm, dpos, dcur, wn, bn, cnt_next, m->ph);
+    else if (nm + cnt_next <= ZG_PH_WIDE_ITEMS)
+      launch_level<ZG_TREE_SAPLING, ZG_PH_LANES_WIDE>(st, L[l], l, nm, dpos, dcur, wn, bn, cnt_next, m->ph);
     else
-      launch_level<ZG_TREE_SPROUT>(st, L[l], l, nm, dpos, dcur, top ? nullptr : wbuf[l + 1],
-                                   top ? 0 : L[l + 1].base, cnt_next, m->ph);
+      launch_level<ZG_TREE_SAPLING, ZG_PH_LANES_NARROW>(st, L[l], l, nm, dpos, dcur, wn, bn, cnt_next, m->ph);
     MCHK(hipGetLastError());
   }
   if (kernel_ms) MCHK(hipEventRecord(e1, st));
