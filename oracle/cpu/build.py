@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Build oracle/_build/libzgcpu.so (the CPU restatement of bellman's per-proof path) with
+"""Build oracle/_build/libzgcpu.so (the CPU restatement of bellman's per-proof path) and
+oracle/_build/libzgmerkle.so (the reference's note-commitment tree path, merkle_cpu.cpp) with
 g++ -O3. Test/bench infrastructure only."""
 import os
 import subprocess
@@ -10,13 +11,26 @@ SRC = os.path.join(HERE, "bellman_cpu.cpp")
 LIB = os.path.join(OUT, "libzgcpu.so")
 
 
-def build():
+MERKLE_SRC = os.path.join(HERE, "merkle_cpu.cpp")
+MERKLE_LIB = os.path.join(OUT, "libzgmerkle.so")
+
+
+def _gxx(src, lib):
     os.makedirs(OUT, exist_ok=True)
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+    if not os.path.exists(lib) or os.path.getmtime(lib) < os.path.getmtime(src):
         subprocess.check_call(["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-shared", "-pthread",
-                               SRC, "-o", LIB + ".tmp"])
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+                               src, "-o", lib + ".tmp"])
+        os.replace(lib + ".tmp", lib)
+    return lib
+
+
+def build():
+    _gxx(MERKLE_SRC, MERKLE_LIB)
+    return _gxx(SRC, LIB)
+
+
+def build_merkle():
+    return _gxx(MERKLE_SRC, MERKLE_LIB)
 
 
 if __name__ == "__main__":

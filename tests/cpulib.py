@@ -37,3 +37,31 @@ def verify(L, proofs, kinds, inputs, n_inputs=None, threads=1, want_gt=False):
                           bytes(n_inputs) if n_inputs is not None else None, st, gts, threads) == 0
     sts = list(st.raw[:n])
     return sts, ([gts.raw[576 * i:576 * i + 576] for i in range(n)] if want_gt else None)
+
+
+def load_merkle():
+    """oracle/_build/libzgmerkle.so (merkle_cpu.cpp), initialised with the Pedersen generators of
+    the Python oracle"""
+    from oracle import merkle as M
+    from oracle.sapling_sig import aff
+    lib = runpy.run_path(os.path.join(ROOT, "oracle", "cpu", "build.py"))["build_merkle"]()
+    L = ctypes.CDLL(lib)
+    L.mc_init.argtypes = [ctypes.c_char_p]
+    L.mc_combine.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
+    L.mc_window.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t,
+                            ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p]
+    gens = b""
+    for j in range(3):
+        x, y = aff(M.pedersen_generator(j))
+        gens += x.to_bytes(32, "little") + y.to_bytes(32, "little")
+    assert L.mc_init(gens) == 0
+    return L
+
+
+def merkle_window(L, kind, height, state, leaves, marks):
+    """mc_window: the reference's sequential appends + roots (marks sorted)"""
+    nm = len(marks)
+    mk = (ctypes.c_uint64 * max(nm, 1))(*marks)
+    out = ctypes.create_string_buffer(max(32 * nm, 1))
+    rc = L.mc_window(kind, height, bytes(state), len(state), len(leaves), b"".join(leaves), nm, mk, out)
+    return rc, [out.raw[32 * k:32 * k + 32] for k in range(nm)]

@@ -30,14 +30,14 @@ void zgt_fr_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
 }
 // binary-GCD inverse on a plain residue (Fr: LE 32 bytes, Fq: BE 48 bytes)
 void zgt_fr_inv_vt(const uint8_t* a, uint8_t* out) {
-  Fr r = fp_inv_vt<FrM, 17>(fr_limbs_from_le(a));
+  Fr r = fp_inv_vt<FrM, ZG_INV_T_FR>(fr_limbs_from_le(a));
   memcpy(out, r.l, 32);
 }
 void zgt_fr_inv_vt_mont(const uint8_t* a, uint8_t* out) {
   Fr r = fr_from_mont(fr_inv_vt(fr_to_mont(fr_limbs_from_le(a))));
   memcpy(out, r.l, 32);
 }
-void zgt_fq_inv_vt(const uint8_t* a, uint8_t* out) { fq_limbs_to_be(fp_inv_vt<FqM, 25>(fq_limbs_from_be(a)), out); }
+void zgt_fq_inv_vt(const uint8_t* a, uint8_t* out) { fq_limbs_to_be(fp_inv_vt<FqM, ZG_INV_T_FQ>(fq_limbs_from_be(a)), out); }
 void zgt_f12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   f12_to_bytes(f12_mul(f12_from_bytes(a), f12_from_bytes(b)), out);
 }

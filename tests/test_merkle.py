@@ -105,3 +105,31 @@ def test_window_roots_matches_appends():
     for h in leaves[5:]:
         t.append(h)
     assert fin.root() == t.root() and fin.serialize() == t.serialize()
+
+
+def test_cpu_port_matches_oracle():
+    """oracle/cpu/merkle_cpu.cpp (the bench's cpu_baseline for trees: the reference's algorithm in
+    C++) against the Python oracle: combine for both trees, the golden empty roots, a window"""
+    from tests import cpulib
+    import ctypes
+    L = cpulib.load_merkle()
+    rnd = random.Random(12)
+    out = ctypes.create_string_buffer(32)
+    for kind, n in ((M.SPROUT, 50), (M.SAPLING, 12)):
+        for _ in range(n):
+            a, b, d = bytes(rnd.getrandbits(8) for _ in range(32)), bytes(rnd.getrandbits(8) for _ in range(32)), rnd.randrange(63)
+            assert L.mc_combine(kind, a, b, d, out) == 0
+            assert out.raw == M.combine(kind, a, b, d)
+    for case in GOLDEN["cases"]:
+        kind, h = KINDS[case["kind"]], case["height"]
+        leaves = [bytes.fromhex(x) for x in case["leaves"]][:case.get("full_after", 99)]
+        marks = list(range(1, len(leaves) + 1)) if "roots" in case else [len(leaves)]
+        rc, roots = cpulib.merkle_window(L, kind, h, b"", leaves, marks)
+        assert rc == 0
+        assert [r.hex() for r in roots] == case.get("roots", [case.get("final_root")])
+    st = M.TreeState(M.SAPLING, 32)
+    for _ in range(5):
+        st.append(bytes(rnd.getrandbits(8) for _ in range(32)))
+    leaves = [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(4)]
+    rc, roots = cpulib.merkle_window(L, M.SAPLING, 32, st.serialize(), leaves, [1, 4])
+    assert rc == 0 and roots == M.window_roots(st, leaves, [1, 4])[0]

@@ -10,8 +10,9 @@ frontier upload, the 32 level launches, the roots' and state's download.
     python tools/bench_tree.py [--reps K] [--leaves N] [--per-block B]
 
 Prints one JSON object: per tree, leaves/s, roots/s, hashes/s (n + HEIGHT x roots + level
-overhang), wall ms per window, the level kernels' device ms (HIP events), and the CPU oracle's
-hash rate for scale (Python, one core; the reference's own Rust is not buildable here).
+overhang), wall ms per window, the level kernels' device ms (HIP events), and the CPU baseline:
+the reference's sequential algorithm restated in C++ (oracle/cpu/merkle_cpu.cpp, one core; the
+reference's own Rust is not buildable here) on windows of the same shape.
 """
 import argparse
 import json
@@ -69,15 +70,27 @@ def run(ctx, kind, height, n, per, reps, warm=2, seed=1):
             "hashes_per_s": h / dt, "kernel_hashes_per_s": h / (kmean * 1e-3)}
 
 
-def cpu_rate(kind, seconds=3.0):
-    from oracle import merkle as M
-    rnd = random.Random(2)
-    a, b = rnd.randbytes(32), rnd.randbytes(32)
-    k, t = 0, time.perf_counter()
+def cpu_window(kind, height, per, seconds=6.0):
+    """the reference's sequential path (oracle/cpu/merkle_cpu.cpp: TreeState append + root per
+    block, sapling-crypto's Pedersen algorithm) on one core, over windows of the same shape
+    (a root per `per` leaves) from the same kind of deep frontier, for about `seconds`"""
+    from tests import cpulib
+    L = cpulib.load_merkle()
+    rnd = random.Random(5 + kind)
+    s0 = (1 << 30) + rnd.randrange(1 << 20)
+    st = frontier(rnd, kind, height, s0).serialize()
+    n = 16 * per
+    leaves = [rnd.randbytes(31) + b"\x00" for _ in range(n)]
+    marks = list(range(per, n + 1, per))
+    done, t = 0, time.perf_counter()
     while time.perf_counter() - t < seconds:
-        a = M.combine(kind, a, b, k % 32)
-        k += 1
-    return k / (time.perf_counter() - t)
+        rc, _ = cpulib.merkle_window(L, kind, height, st, leaves, marks)
+        assert rc == 0
+        done += 1
+    dt = time.perf_counter() - t
+    return {"leaves_per_s": done * n / dt, "roots_per_s": done * len(marks) / dt, "cores": 1, "kind": "port",
+            "sample": "%d windows of %d leaves, a root per %d, from a 2^30-leaf frontier (%.1f s)"
+                      % (done, n, per, dt)}
 
 
 def main():
@@ -97,8 +110,8 @@ def main():
     out["sapling_h32"] = run(ctx, zg.TREE_SAPLING, 32, a.leaves, a.per_block, a.reps)
     out["sprout_h29"] = run(ctx, zg.TREE_SPROUT, 29, a.leaves, a.per_block, a.reps)
     if not a.no_cpu:
-        out["cpu_oracle_hashes_per_s"] = {"sapling": cpu_rate(zg.TREE_SAPLING), "sprout": cpu_rate(zg.TREE_SPROUT),
-                                          "kind": "port (Python oracle, 1 core)"}
+        out["sapling_h32"]["cpu_baseline"] = cpu_window(zg.TREE_SAPLING, 32, a.per_block)
+        out["sprout_h29"]["cpu_baseline"] = cpu_window(zg.TREE_SPROUT, 29, a.per_block)
     ctx.close()
     print(json.dumps(out))
 

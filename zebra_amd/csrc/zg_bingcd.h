@@ -1,17 +1,21 @@
 // zg_bingcd.h -- variable-time modular inversion by binary GCD with 64-bit approximations
-// (T. Pornin, "Optimized Binary GCD for Modular Inversion", 2020, algorithm 2, k = 31).
+// (T. Pornin, "Optimized Binary GCD for Modular Inversion", 2020, algorithm 2; here 30 divsteps
+// per outer step on 64-bit approximations).
 //
 // For PUBLIC values only (tree hashes, decoded points): the running time depends on the input.
 // It replaces Fermat's a^(p-2) (log2 p squarings + multiplications, ~380 Fr products) where an
-// inversion sits on a latency-critical chain: 17 outer steps (Fr) of 31 divsteps on 64-bit
-// approximations of a and b (their low 31 and top 33 bits), each followed by one linear update
-// of the full a, b (exact division by 2^31) and of the Bezout pair u, v (Montgomery division by
-// 2^31, so that a = y u and b = y v mod p hold throughout). 2 len(p) - 1 divsteps suffice for
+// inversion sits on a latency-critical chain: 17 outer steps (Fr) of 30 divsteps on 64-bit
+// approximations of a and b (their low 30 and top 34 bits), each followed by one linear update
+// of the full a, b (exact division by 2^30) and of the Bezout pair u, v (Montgomery division by
+// 2^30, so that a = y u and b = y v mod p hold throughout). 2 len(p) - 1 divsteps suffice for
 // b to reach gcd(y, p) = 1 (then v = y^-1); y = 0 returns 0, as a^(p-2) does.
 #pragma once
 #include "zg_field.h"
 
 namespace zg {
+
+#define ZG_INV_T_FR 17  // ceil((2 * 255 - 1) / 30)
+#define ZG_INV_T_FQ 26  // ceil((2 * 381 - 1) / 30)
 
 // acc (N + 2 limbs, two's complement) += (neg ? -1 : 1) * a * m, a unsigned N limbs, m < 2^32
 template <int N>
@@ -34,12 +38,12 @@ ZG_INL void bg_mac(uint32_t* acc, const uint32_t* a, uint32_t m, bool neg) {
   }
 }
 
-// t (N + 2 limbs, two's complement) >>= 31, arithmetic
-template <int N>
-ZG_INL void bg_shr31(uint32_t* t) {
+// t (N + 2 limbs, two's complement) >>= S (0 < S < 32), arithmetic
+template <int N, int S>
+ZG_INL void bg_shr(uint32_t* t) {
 #pragma unroll
-  for (int i = 0; i < N + 1; i++) t[i] = (t[i] >> 31) | (t[i + 1] << 1);
-  t[N + 1] = (uint32_t)((int32_t)t[N + 1] >> 31);
+  for (int i = 0; i < N + 1; i++) t[i] = (t[i] >> S) | (t[i + 1] << (32 - S));
+  t[N + 1] = (uint32_t)((int32_t)t[N + 1] >> S);
 }
 
 template <int N>
@@ -102,10 +106,14 @@ ZG_INL uint64_t bg_bits64(const uint32_t* a, int off) {
   return sh ? (x >> sh) | (hi << (64 - sh)) : x;
 }
 
-// y^-1 mod p for a residue y in [0, p) (any representation: the caller fixes Montgomery factors)
+// y^-1 mod p for a residue y in [0, p) (any representation: the caller fixes Montgomery factors).
+// T outer steps of 30 divsteps each, T * 30 >= 2 len(p) - 1 (Fr: 17, Fq: 26). The update
+// factors of one outer step stay within [-2^30, 2^30], so each pair (f, g) travels packed in one
+// 64-bit word f + 2^32 g (the divsteps are linear in it) and is unpacked once per step.
 template <class M, int T>
 ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
   constexpr int N = M::N;
+  constexpr int K = 30;
   uint32_t a[N], b[N], u[N], v[N];
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -119,24 +127,25 @@ ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
     const int nb = bg_bitlen<N>(b);
     n = n > nb ? n : nb;
     n = n > 64 ? n : 64;
-    const uint64_t low = (1ull << 31) - 1;
-    uint64_t xa = ((uint64_t)a[0] & low) | ((bg_bits64<N>(a, n - 33) & ((1ull << 33) - 1)) << 31);
-    uint64_t xb = ((uint64_t)b[0] & low) | ((bg_bits64<N>(b, n - 33) & ((1ull << 33) - 1)) << 31);
-    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
-#pragma unroll 4
-    for (int j = 0; j < 31; j++) {
+    // low K bits and top 64 - K bits of a and b
+    const uint64_t low = (1ull << K) - 1;
+    uint64_t xa = ((uint64_t)a[0] & low) | (bg_bits64<N>(a, n - (64 - K)) << K);
+    uint64_t xb = ((uint64_t)b[0] & low) | (bg_bits64<N>(b, n - (64 - K)) << K);
+    uint64_t p0 = 1, p1 = 1ull << 32;  // (f0, g0) = (1, 0), (f1, g1) = (0, 1)
+#pragma unroll 6
+    for (int j = 0; j < K; j++) {
       const bool odd = xa & 1;
       const bool sw = odd && xa < xb;
       const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
-      const int64_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
-      xa = (odd ? ta - tb : ta) >> 1;
+      const uint64_t tp0 = sw ? p1 : p0, tp1 = sw ? p0 : p1;
+      xa = (ta - (odd ? tb : 0)) >> 1;
       xb = tb;
-      f0 = odd ? tf0 - tf1 : tf0;
-      g0 = odd ? tg0 - tg1 : tg0;
-      f1 = tf1 << 1;
-      g1 = tg1 << 1;
+      p0 = tp0 - (odd ? tp1 : 0);
+      p1 = tp1 << 1;
     }
-    // (a, b) <- ((a f0 + b g0) / 2^31, (a f1 + b g1) / 2^31), signs folded into the factors
+    int64_t f0 = (int32_t)(uint32_t)p0, f1 = (int32_t)(uint32_t)p1;
+    int64_t g0 = ((int64_t)p0 - f0) >> 32, g1 = ((int64_t)p1 - f1) >> 32;
+    // (a, b) <- ((a f0 + b g0) / 2^K, (a f1 + b g1) / 2^K), signs folded into the factors
     uint32_t na[N + 2], nb2[N + 2];
 #pragma unroll
     for (int i = 0; i < N + 2; i++) na[i] = nb2[i] = 0;
@@ -144,25 +153,22 @@ ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
     bg_mac<N>(na, b, (uint32_t)(g0 < 0 ? -g0 : g0), g0 < 0);
     bg_mac<N>(nb2, a, (uint32_t)(f1 < 0 ? -f1 : f1), f1 < 0);
     bg_mac<N>(nb2, b, (uint32_t)(g1 < 0 ? -g1 : g1), g1 < 0);
-    bg_shr31<N>(na);
-    bg_shr31<N>(nb2);
+    bg_shr<N, K>(na);
+    bg_shr<N, K>(nb2);
     const bool fa = bg_neg_p<N>(na), fb = bg_neg_p<N>(nb2);
     bg_cneg<N>(na, fa);
     bg_cneg<N>(nb2, fb);
-    if (fa) {
-      f0 = -f0;
-      g0 = -g0;
-    }
-    if (fb) {
-      f1 = -f1;
-      g1 = -g1;
-    }
+    f0 = fa ? -f0 : f0;
+    g0 = fa ? -g0 : g0;
+    f1 = fb ? -f1 : f1;
+    g1 = fb ? -g1 : g1;
 #pragma unroll
     for (int i = 0; i < N; i++) {
       a[i] = na[i];
       b[i] = nb2[i];
     }
-    // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31) mod p (Montgomery division)
+    // (u, v) <- ((u f0 + v g0) / 2^K, (u f1 + v g1) / 2^K) mod p (Montgomery division): with
+    // |f0| + |g0| <= 2^K and u, v < p the quotient lies in (-p, 2p)
     uint32_t nu[N + 2], nv[N + 2];
 #pragma unroll
     for (int i = 0; i < N + 2; i++) nu[i] = nv[i] = 0;
@@ -173,18 +179,13 @@ ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
     uint32_t pm[N];
 #pragma unroll
     for (int i = 0; i < N; i++) pm[i] = M::p(i);
-    bg_mac<N>(nu, pm, (nu[0] * M::INV) & 0x7fffffffu, false);
-    bg_mac<N>(nv, pm, (nv[0] * M::INV) & 0x7fffffffu, false);
-    bg_shr31<N>(nu);
-    bg_shr31<N>(nv);
-    // now in (-3p, 3p): into [0, p)
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-      bg_cadd_p<M>(nu, bg_neg_p<N>(nu), false);
-      bg_cadd_p<M>(nv, bg_neg_p<N>(nv), false);
-    }
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
+    bg_mac<N>(nu, pm, (nu[0] * M::INV) & (uint32_t)low, false);
+    bg_mac<N>(nv, pm, (nv[0] * M::INV) & (uint32_t)low, false);
+    bg_shr<N, K>(nu);
+    bg_shr<N, K>(nv);
+    bg_cadd_p<M>(nu, bg_neg_p<N>(nu), false);
+    bg_cadd_p<M>(nv, bg_neg_p<N>(nv), false);
+    {
       uint32_t tu[N + 2], tv[N + 2];
 #pragma unroll
       for (int i = 0; i < N + 2; i++) {
@@ -195,15 +196,10 @@ ZG_INL Fp<M> fp_inv_vt(const Fp<M>& y) {
       bg_cadd_p<M>(tv, true, true);
       const bool ku = !bg_neg_p<N>(tu), kv = !bg_neg_p<N>(tv);
 #pragma unroll
-      for (int i = 0; i < N + 2; i++) {
-        nu[i] = ku ? tu[i] : nu[i];
-        nv[i] = kv ? tv[i] : nv[i];
+      for (int i = 0; i < N; i++) {
+        u[i] = ku ? tu[i] : nu[i];
+        v[i] = kv ? tv[i] : nv[i];
       }
-    }
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-      u[i] = nu[i];
-      v[i] = nv[i];
     }
   }
   // b == 1 unless y == 0 (then v == 0 too)
@@ -218,7 +214,7 @@ ZG_INL Fr fr_inv_vt(const Fr& a) {
   Fr r3;
 #pragma unroll
   for (int i = 0; i < 8; i++) r3.l[i] = FR_R3[i];
-  return fr_mul(fp_inv_vt<FrM, 17>(a), r3);
+  return fr_mul(fp_inv_vt<FrM, ZG_INV_T_FR>(a), r3);
 }
 
 }  // namespace zg
