@@ -422,6 +422,17 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_configs:
         out["other_configs"] = other_configs(ctx, src_proofs, src_kinds)
+        # note-commitment tree windows (tools/bench_tree.py), not the headline
+        from tools import bench_tree
+        from zebra_amd import zg as _zg
+        trees = {"workload": "1,024 blocks x 64 commitments (65,536 leaves, a root per block) onto a "
+                             "2^30-leaf frontier, leaves HBM-resident (zg_tree_roots_device)"}
+        for name, kind, h in (("sapling_h32", _zg.TREE_SAPLING, 32), ("sprout_h29", _zg.TREE_SPROUT, 29)):
+            trees[name] = bench_tree.run(ctx, kind, h, 65536, 64, 10)
+            if not args.no_cpu:
+                trees[name]["cpu_baseline"] = bench_tree.cpu_window(kind, h, 64, 4.0)
+                trees[name]["gpu_over_cpu"] = trees[name]["leaves_per_s"] / trees[name]["cpu_baseline"]["leaves_per_s"]
+        out["note_commitment_trees"] = trees
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(proofs, kinds, inputs, args.cpu_seconds, cpu_threads(args.cpu_threads))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -42,7 +42,7 @@ size_t merkle_state_max_bytes(int height);
 int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const uint8_t* state, size_t state_len,
                       size_t n, const void* leaves, int leaves_on_device, size_t nmarks, const uint64_t* marks,
                       uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms,
-                      std::string* err);
+                      void** arena, size_t* arena_cap, std::string* err);
 }  // namespace zg
 
 // Per-device state shared by every context (batch slot) on that GPU: a FIXED pool of stream
@@ -132,6 +132,8 @@ struct zg_ctx {
   // [6] K4 bucket entries of the last batch (points with a non-zero digit, summed over windows)
   uint64_t stats[ZG_NSTATS] = {};
   uint64_t calls = 0;
+  void* tree_arena = nullptr;  // zg_tree_roots scratch (grow-only, zg_merkle.hip)
+  size_t tree_arena_cap = 0;
 };
 
 static int fail(zg_ctx* c, int code, const std::string& msg) {
@@ -296,7 +298,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
-                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart};
+                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -1391,7 +1393,8 @@ static int tree_roots(zg_ctx* ctx, int kind, int height, const uint8_t* state, s
   std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   return merkle_tree_roots(merkle_dev(ctx), ctx->stream, kind, height, state, state_len, n, leaves, on_device,
-                           n_marks, marks, roots, state_out, state_out_len, kernel_ms, &ctx->err);
+                           n_marks, marks, roots, state_out, state_out_len, kernel_ms, &ctx->tree_arena,
+                           &ctx->tree_arena_cap, &ctx->err);
 }
 
 extern "C" int zg_tree_roots(zg_ctx* ctx, int kind, int height, const uint8_t* state, size_t state_len,

@@ -299,7 +299,7 @@ static void launch_level(hipStream_t st, const TreeLevel& L, int level, int nm, 
 int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const uint8_t* state, size_t state_len,
                       size_t n, const void* leaves, int leaves_on_device, size_t nmarks, const uint64_t* marks,
                       uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms,
-                      std::string* err) {
+                      void** arena, size_t* arena_cap, std::string* err) {
   if (height < 1 || height > 62 || (kind != ZG_TREE_SPROUT && kind != ZG_TREE_SAPLING)) return ZG_E_INVAL;
   HostTree t;
   t.phas.assign(height - 1, 0);
@@ -335,37 +335,14 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
   const unsigned long long n_eff = std::min<unsigned long long>(n, capacity - s0);
   const unsigned long long s1 = s0 + n_eff;
 
-  Scratch s;
-  // frontier slots: [0] leaf s0 - 1, [1] leaf s0 - 2, [2 + i] parents[i] (level i + 1)
-  std::vector<uint8_t> fh(32 * (2 + height), 0);
-  if (s0) {
-    const bool even = (s0 & 1) == 0;
-    memcpy(&fh[0], even ? t.lr[1] : t.lr[0], 32);
-    if (even) memcpy(&fh[32], t.lr[0], 32);
-  }
-  for (int i = 0; i < height - 1; i++)
-    if (t.phas[i]) memcpy(&fh[32 * (2 + i)], t.par[i].data(), 32);
-  uint32_t* dfront;
-  MCHK(s.alloc(&dfront, fh.size()));
-  MCHK(hipMemcpyAsync(dfront, fh.data(), fh.size(), hipMemcpyHostToDevice, st));
-  const uint32_t* dleaves = (const uint32_t*)leaves;
-  if (!leaves_on_device && n_eff) {
-    uint32_t* dl;
-    MCHK(s.alloc(&dl, 32 * n_eff));
-    MCHK(hipMemcpyAsync(dl, leaves, 32 * n_eff, hipMemcpyHostToDevice, st));
-    dleaves = dl;
-  }
-  const uint32_t* E = m->empty[kind];
-  // level descriptors
-  std::vector<TreeLevel> L(height);
-  L[0] = {dleaves, (long long)s0, (long long)n_eff, dfront, dfront + 8, E};
-  std::vector<uint32_t*> wbuf(height, nullptr);
+  // level extents (W_l holds nodes base .. base + cnt - 1 of level l)
+  std::vector<long long> lbase(height, 0), lcnt(height, 0);
+  lbase[0] = (long long)s0;
+  lcnt[0] = (long long)n_eff;
   for (int l = 1; l < height; l++) {
-    const long long base = s0 ? (long long)((s0 - 1) >> l) : 0;
+    lbase[l] = s0 ? (long long)((s0 - 1) >> l) : 0;
     const long long last = s1 ? (long long)((s1 - 1) >> l) : -1;
-    const long long cnt = std::max(0ll, last - base + 1);
-    MCHK(s.alloc(&wbuf[l], 32 * (size_t)cnt));
-    L[l] = {wbuf[l], base, cnt, dfront + 8 * (2 + (l - 1)), nullptr, E + 8 * l};
+    lcnt[l] = std::max(0ll, last - lbase[l] + 1);
   }
   // root walks: marks with at least one leaf and within capacity
   std::vector<unsigned long long> pos;
@@ -383,10 +360,53 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
     }
   }
   const int nm = (int)pos.size();
-  unsigned long long* dpos = nullptr;
-  uint32_t* dcur = nullptr;
-  MCHK(s.alloc(&dpos, sizeof(unsigned long long) * (nm ? nm : 1)));
-  MCHK(s.alloc(&dcur, 32 * (size_t)(nm ? nm : 1)));
+  // one device allocation per context, reused across calls (grow-only, zg_destroy frees it)
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  size_t need = al(32 * (2 + (size_t)height)) + (leaves_on_device ? 0 : al(32 * n_eff)) +
+                al(sizeof(unsigned long long) * (nm + 1)) + al(32 * (size_t)(nm + 1)) +
+                2 * al(32 * (size_t)(height + 1));
+  for (int l = 1; l < height; l++) need += al(32 * (size_t)lcnt[l]);
+  if (*arena_cap < need) {
+    if (*arena) hipFree(*arena);
+    *arena = nullptr;
+    *arena_cap = 0;
+    MCHK(hipMalloc(arena, need));
+    *arena_cap = need;
+  }
+  char* bump = (char*)*arena;
+  auto take = [&](size_t b) {
+    char* p = bump;
+    bump += al(b);
+    return (void*)p;
+  };
+  // frontier slots: [0] leaf s0 - 1, [1] leaf s0 - 2, [2 + i] parents[i] (level i + 1)
+  std::vector<uint8_t> fh(32 * (2 + height), 0);
+  if (s0) {
+    const bool even = (s0 & 1) == 0;
+    memcpy(&fh[0], even ? t.lr[1] : t.lr[0], 32);
+    if (even) memcpy(&fh[32], t.lr[0], 32);
+  }
+  for (int i = 0; i < height - 1; i++)
+    if (t.phas[i]) memcpy(&fh[32 * (2 + i)], t.par[i].data(), 32);
+  uint32_t* dfront = (uint32_t*)take(fh.size());
+  MCHK(hipMemcpyAsync(dfront, fh.data(), fh.size(), hipMemcpyHostToDevice, st));
+  const uint32_t* dleaves = (const uint32_t*)leaves;
+  if (!leaves_on_device) {
+    uint32_t* dl = (uint32_t*)take(32 * n_eff);
+    if (n_eff) MCHK(hipMemcpyAsync(dl, leaves, 32 * n_eff, hipMemcpyHostToDevice, st));
+    dleaves = dl;
+  }
+  const uint32_t* E = m->empty[kind];
+  // level descriptors
+  std::vector<TreeLevel> L(height);
+  L[0] = {dleaves, lbase[0], lcnt[0], dfront, dfront + 8, E};
+  std::vector<uint32_t*> wbuf(height, nullptr);
+  for (int l = 1; l < height; l++) {
+    wbuf[l] = (uint32_t*)take(32 * (size_t)lcnt[l]);
+    L[l] = {wbuf[l], lbase[l], lcnt[l], dfront + 8 * (2 + (l - 1)), nullptr, E + 8 * l};
+  }
+  unsigned long long* dpos = (unsigned long long*)take(sizeof(unsigned long long) * (nm + 1));
+  uint32_t* dcur = (uint32_t*)take(32 * (size_t)(nm + 1));
   if (nm) MCHK(hipMemcpyAsync(dpos, pos.data(), sizeof(unsigned long long) * nm, hipMemcpyHostToDevice, st));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (kernel_ms) {
@@ -438,10 +458,8 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
   }
   std::vector<uint8_t> fr(32 * src.size());
   if (!src.empty() && state_out && !full) {
-    const uint32_t** dsrc;
-    uint32_t* dout;
-    MCHK(s.alloc(&dsrc, sizeof(void*) * src.size()));
-    MCHK(s.alloc(&dout, fr.size()));
+    const uint32_t** dsrc = (const uint32_t**)take(sizeof(void*) * src.size());
+    uint32_t* dout = (uint32_t*)take(fr.size());
     MCHK(hipMemcpyAsync(dsrc, src.data(), sizeof(void*) * src.size(), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_gather32, dim3(blocks64(8 * (long long)src.size())), dim3(64), 0, st, (int)src.size(),
                        (const uint32_t* const*)dsrc, dout);
