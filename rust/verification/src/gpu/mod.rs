@@ -188,6 +188,27 @@ impl GpuVerifier {
         })?;
         Ok((0..n).map(|i| (st[i], bvk[32 * i..32 * i + 32].try_into().unwrap())).collect())
     }
+
+    /// Note-commitment tree roots over an import window (storage::TreeState, serialized as the
+    /// reference stores it): from `state` (empty = TreeState::new()) append `leaves` and return the
+    /// root after each `marks[k]` of them (one per block for BlockSaplingRoot / the Sprout block
+    /// root, one per JoinSplit for TreeCache::continue_root) and the serialized final state.
+    /// kind: ffi::ZG_TREE_SPROUT (H29) or ffi::ZG_TREE_SAPLING (H32). Err(ZG_E_TREE_FULL) when the
+    /// leaves overflow the tree ("Appending to full tree").
+    pub fn tree_roots(&self, kind: c_int, height: c_int, state: &[u8], leaves: &[[u8; 32]], marks: &[u64])
+                      -> Result<(Vec<[u8; 32]>, Vec<u8>), GpuError> {
+        let _g = self.lock.lock().unwrap();
+        let flat: Vec<u8> = leaves.iter().flat_map(|h| h.iter().copied()).collect();
+        let mut roots = vec![0u8; 32 * marks.len()];
+        let mut out_len = unsafe { ffi::zg_tree_state_max_bytes(height) };
+        let mut out = vec![0u8; out_len];
+        check(self.ctx, unsafe {
+            ffi::zg_tree_roots(self.ctx, kind, height, state.as_ptr(), state.len(), leaves.len(), flat.as_ptr(),
+                               marks.len(), marks.as_ptr(), roots.as_mut_ptr(), out.as_mut_ptr(), &mut out_len)
+        })?;
+        out.truncate(out_len);
+        Ok((roots.chunks(32).map(|c| c.try_into().unwrap()).collect(), out))
+    }
 }
 
 impl Drop for GpuVerifier {
