@@ -561,6 +561,115 @@ def gen_tree_state():
     print("wrote tree_state.json", len(out["sprout_empty"]), len(out["sapling_empty"]), len(cases), "cases")
 
 
+def gen_pghr13():
+    """pghr13.json: PGHR13 (BN254) proofs from the reference's tests and mainnet blocks with the
+    oracle's verdicts: crypto/src/pghr13.rs proof_decode / verification /
+    verification2, verification/src/sprout.rs smoky_pghr, the PHGR JoinSplits of blocks 522 and
+    567 (test-data/src/lib.rs:97-110); plus encoding / subgroup / statement mutants"""
+    from oracle import bn254 as BN, pghr13 as PG
+    vk = PG.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", "sprout-verifying-key.json")).read())
+    src = open(os.path.join(REF, "crypto/src/pghr13.rs")).read()
+    sample = bytes.fromhex(re.search(r'pgh13_proof\("([0-9a-f]{592})"\)', src).group(1))
+
+    def pts_from(body):
+        n = [int(x) for x in re.findall(r'from_str\("(\d+)"\)', body)]
+        pt = {"a": (n[0], n[1]), "a_prime": (n[2], n[3]), "b": ((n[4], n[5]), (n[6], n[7])),
+              "b_prime": (n[8], n[9]), "c": (n[10], n[11]), "c_prime": (n[12], n[13]),
+              "h": (n[14], n[15]), "k": (n[16], n[17])}
+        return pt, n[18:]
+
+    dec_pt, _ = pts_from(src[src.index("fn proof_decode()"):src.index("fn verification()")])
+    assert PG.proof_from_raw(sample) == dec_pt
+    cases = []
+
+    def add(name, proof, inputs, want=None):
+        st = PG.verify_raw(vk, proof, inputs)
+        if want is not None:
+            assert st == want, (name, st)
+        cases.append({"name": name, "proof": proof.hex(), "inputs": [x.to_bytes(32, "little").hex() for x in inputs],
+                      "status": st})
+        print(name, st, flush=True)
+
+    for fn, nxt in (("fn verification()", "fn verification2()"), ("fn verification2()", None)):
+        body = src[src.index(fn):src.index(nxt) if nxt else len(src)]
+        pt, inputs = pts_from(body)
+        add(fn[3:-2], PG.proof_to_raw(pt), inputs, PG.OK)
+    spr = open(os.path.join(REF, "verification/src/sprout.rs")).read()
+    body = spr[spr.index("fn smoky_pghr()"):spr.index("fn sample_groth_proof()")]
+    h2 = re.findall(r'hash2\("([0-9a-f]{64})"\)', body)
+    desc = {"vpub_new": int(re.search(r"value_pub_new: (\d+)", body).group(1)),
+            "vpub_old": int(re.search(r"value_pub_old: (\d+)", body).group(1)),
+            "anchor": bytes.fromhex(h2[0]), "nullifiers": [bytes.fromhex(h2[1]), bytes.fromhex(h2[2])],
+            "commitments": [bytes.fromhex(h2[3]), bytes.fromhex(h2[4])], "random_seed": bytes.fromhex(h2[5]),
+            "macs": [bytes.fromhex(h2[6]), bytes.fromhex(h2[7])]}
+    pubkey = bytes.fromhex(h2[8])
+    add("smoky_pghr", sample, PG.joinsplit_inputs(desc, pubkey), PG.OK)
+    lib = open(os.path.join(REF, "test-data/src/lib.rs")).read()
+    for fn in ("pub fn block_h522()", "pub fn block_h567()"):
+        seg = lib[lib.index(fn):]
+        hx_ = re.search(r'"([0-9a-f]{200,})"', seg[:seg.index("\n}\n")]).group(1)
+        _, txs = Z.parse_block_hex(hx_)
+        k = 0
+        for t in txs:
+            for d in t["joinsplits"]:
+                if not d["groth"]:
+                    add("%s_tx%s_js%d" % (fn.split("_")[1][:-2], t["txid"][:8], k), d["zkproof"],
+                        PG.joinsplit_inputs(d, t["js_pubkey"]), PG.OK)
+                    k += 1
+    # mutants of the sample statement (sprout.rs smoky_pghr)
+    base = sample
+    base_in = PG.joinsplit_inputs(desc, pubkey)
+
+    def mut(name, b, inputs=None, want=None):
+        add("mut_" + name, bytes(b), base_in if inputs is None else inputs, want)
+
+    b = bytearray(base); b[0] ^= 1; mut("a_sign", b, want=PG.INVALID_PROOF)          # -a
+    b = bytearray(base); b[66] ^= 1; mut("b_sign", b, want=PG.INVALID_PROOF)         # -b
+    b = bytearray(base); b[263] ^= 1; mut("h_sign", b, want=PG.INVALID_PROOF)
+    b = bytearray(base); b[33] = 4; mut("a_prime_prefix", b, want=PG.INVALID_ENCODING)
+    b = bytearray(base); b[66] = 2; mut("b_prefix", b, want=PG.INVALID_ENCODING)
+    b = bytearray(base); b[164 + 1:164 + 33] = (BN.P + 5).to_bytes(32, "big"); mut("c_x_ge_p", b, want=PG.INVALID_ENCODING)
+    b = bytearray(base); b[67:131] = (BN.P * BN.P + 1).to_bytes(64, "big"); mut("b_c1_ge_p", b, want=PG.INVALID_ENCODING)
+    # x with no curve point (G1) and twist points outside the order-r subgroup (G2)
+    x = 1
+    while BN.fq_sqrt(x ** 3 + 3) is not None:
+        x += 1
+    b = bytearray(base); b[231:263] = x.to_bytes(32, "big"); mut("k_not_on_curve", b, want=PG.INVALID_ENCODING)
+    x0 = 1
+    while True:
+        xx = (x0, 1)
+        y = BN.f2_sqrt(BN.f2_add(BN.f2_mul(BN.f2_sqr(xx), xx), BN.B2))
+        if y is not None and BN.ec_mul(BN._F2, (xx, y), BN.R) is not None:
+            break
+        x0 += 1
+    b = bytearray(base); b[67:131] = BN.f2_to_u512(xx).to_bytes(64, "big"); mut("b_not_in_subgroup", b,
+                                                                                want=PG.INVALID_ENCODING)
+    for name, off in (("a_x", 1), ("a_prime_x", 34), ("b_prime_x", 132), ("c_prime_x", 198), ("k_x", 231)):
+        for bump in range(1, 40):
+            b = bytearray(base)
+            v = (int.from_bytes(b[off:off + 32], "big") + bump) % BN.P
+            b[off:off + 32] = v.to_bytes(32, "big")
+            try:
+                PG.proof_from_raw(bytes(b))
+            except BN.DecodeError:
+                continue
+            mut(name + "_moved", b, want=PG.INVALID_PROOF)
+            break
+    bad_in = list(base_in)
+    bad_in[3] ^= 1
+    mut("input3", base, bad_in, PG.INVALID_PROOF)
+    mut("short_inputs", base, base_in[:8], PG.INVALID_PROOF)
+    with open(os.path.join(HERE, "pghr13.json"), "w") as f:
+        json.dump({"vk_file": "sprout-verifying-key.json", "sample_proof": sample.hex(),
+                   "sample_points": {k: [list(v) if isinstance(v, tuple) and isinstance(v[0], tuple) else v
+                                         for v in [dec_pt[k]]][0] for k in dec_pt},
+                   "cases": cases,
+                   "source": "crypto/src/pghr13.rs tests, verification/src/sprout.rs smoky_pghr, "
+                             "test-data blocks 522 / 567; mutants by the oracle"},
+                  f, indent=1, sort_keys=True)
+    print("wrote pghr13.json", len(cases), "cases")
+
+
 def refresh_batch_gt():
     """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
     change of the batch-scalar mapping; no reference sources needed)"""
@@ -586,6 +695,8 @@ if __name__ == "__main__":
         gen_vk_codec()
     elif len(sys.argv) > 1 and sys.argv[1] == "--sapling-sigs":
         gen_sapling_sigs()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--pghr13":
+        gen_pghr13()
     elif len(sys.argv) > 1 and sys.argv[1] == "--tree-state":
         gen_tree_state()
     else:

@@ -1,0 +1,57 @@
+"""PGHR13 on BN254: the oracle (oracle/bn254.py, oracle/pghr13.py) against
+the reference's own vectors (tests/golden/pghr13.json: crypto/src/pghr13.rs proof_decode /
+verification tests, sprout.rs smoky_pghr, the PHGR JoinSplits of mainnet block 522), plus the
+pairing's bilinearity."""
+import os
+
+import pytest
+
+from oracle import bn254 as B, pghr13 as PG
+from tests.conftest import ROOT, load_golden
+
+GOLDEN = load_golden("pghr13.json")
+
+
+@pytest.fixture(scope="module")
+def vk():
+    return PG.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", "sprout-verifying-key.json")).read())
+
+
+def test_pairing_is_bilinear_and_non_degenerate():
+    e = B.pairing(B.G1_GEN, B.G2_GEN)
+    assert e != B.F12_ONE and B.f12_pow(e, B.R) == B.F12_ONE
+    assert B.pairing(B.ec_mul(B._F1, B.G1_GEN, 6), B.ec_mul(B._F2, B.G2_GEN, 7)) == B.f12_pow(e, 42)
+
+
+def test_proof_decode_matches_reference():
+    """pghr13.rs proof_decode: the 8 decoded points of the sample proof (both compressed forms,
+    the G2 Fq2 blob layout and y_gt sign rule); and encoding round trips"""
+    pr = PG.proof_from_raw(bytes.fromhex(GOLDEN["sample_proof"]))
+    want = GOLDEN["sample_points"]
+    for k, v in want.items():
+        got = pr[k]
+        if k == "b":
+            assert [list(got[0]), list(got[1])] == v
+        else:
+            assert list(got) == v
+    assert PG.proof_to_raw(pr).hex() == GOLDEN["sample_proof"]
+
+
+def test_vk_points_checked(vk):
+    assert len(vk["ic"]) == 10
+    for k in ("a", "c", "z", "gamma", "gamma_beta_2"):
+        assert B.ec_mul(B._F2, vk[k], B.R) is None
+
+
+@pytest.mark.parametrize("name", ["verification", "smoky_pghr", "mut_b_sign", "mut_b_not_in_subgroup", "mut_input3"])
+def test_oracle_verdicts(vk, name):
+    c = next(c for c in GOLDEN["cases"] if c["name"] == name)
+    inputs = [int.from_bytes(bytes.fromhex(x), "little") for x in c["inputs"]]
+    assert PG.verify_raw(vk, bytes.fromhex(c["proof"]), inputs) == c["status"]
+
+
+def test_fixture_shape():
+    st = {c["name"]: c["status"] for c in GOLDEN["cases"]}
+    real = [n for n in st if n.startswith(("verification", "smoky", "h522"))]
+    assert len(real) == 9 and all(st[n] == PG.OK for n in real)
+    assert {st[n] for n in st if n.startswith("mut_")} == {PG.INVALID_ENCODING, PG.INVALID_PROOF}
