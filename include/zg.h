@@ -231,6 +231,29 @@ int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uint8_t* state
                          size_t n_leaves, const void* d_leaves, size_t n_marks, const uint64_t* marks,
                          uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms);
 
+/* ---- PGHR13 Sprout proofs on BN254: pre-Sapling JoinSplits (the `bn` crate).
+ *   zg_pghr13_vk_load_builtin / _json <- crypto/src/json/pghr13.rs decode of
+ *        res/sprout-verifying-key.json (embedded unchanged); points through AffineG1/G2::new
+ *        (ZG_E_VK when one is off its curve or, in G2, not of order r). zg_pghr13_verify loads
+ *        the builtin key on first use.
+ *   zg_pghr13_verify <- Proof::from_raw + pghr13::verify (crypto/src/pghr13.rs:69-105), called at
+ *        verification/src/sprout.rs:61-67: proofs n x 296 bytes (the JoinSplit's PHGR proof),
+ *        inputs n x 9 x 32 bytes (BN254 Fr, little-endian: Input::into_bn_frs, 253-bit chunks),
+ *        n_inputs optional (count per proof, <= 9; NULL = 9; fewer inputs contribute fewer
+ *        ic terms, as the reference's zip). status n: ZG_STATUS_OK, ZG_STATUS_DECODE_INVALID
+ *        (-> ErrorKind::InvalidEncoding), ZG_STATUS_VERIFY_FAILED (-> InvalidPGHRProof),
+ *        ZG_STATUS_INPUT_NONCANONICAL (an input >= r: not constructible as bn::Fr). The five
+ *        pairing equalities of a proof are checked as one product with OS-random 128-bit weights
+ *        (false accept ~2^-128). kernel_ms optional: device time of the three kernels.
+ *   zg_bn254_pairing (tests): e(P, Q) to the power 2u(6u^2 + 3u + 1) (the device's final
+ *        exponentiation, see zg_bn254.h): P n x 64 (x, y), Q n x 128 (x.c0, x.c1, y.c0, y.c1),
+ *        canonical little-endian Fq; GT n x 384 (12 Fq, coefficients of w^0..w^5 as c0, c1). */
+int zg_pghr13_vk_load_builtin(zg_ctx* ctx);
+int zg_pghr13_vk_load_json(zg_ctx* ctx, const char* json, size_t len);
+int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* inputs, const uint8_t* n_inputs,
+                     uint8_t* status, float* kernel_ms);
+int zg_bn254_pairing(zg_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt);
+
 /* ---- synthetic workload (bench/tests): Groth16 re-randomization of real proofs,
  * out[i] = rerandomize(src[src_index[i]]) with (t, s) = BLAKE2b-512("zg-rerand"||seed||i)
  * (A,B,C) -> (t^-1 A, t B + t s delta, C + s A); valid iff the source is. */

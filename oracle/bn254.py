@@ -399,3 +399,44 @@ def g2_to_compressed(pt):
     x, y = pt
     gt = f2_to_u512(y) > f2_to_u512(f2_neg(y))
     return bytes([11 if gt else 10]) + f2_to_u512(x).to_bytes(64, "big")
+
+
+# ----------------------------------------------------------------------------- the device's final exponentiation
+def f12_exp_by_neg_u(f):
+    return f12_conj(f12_pow(f, U))
+
+
+def final_exponentiation_fc(f):
+    """the addition chain the GPU runs for the hard part (Fuentes-Castaneda, Knapp and
+    Rodriguez-Henriquez; the `bn` crate's final_exponentiation_last_chunk): it raises the
+    easy-part output to 2u(6u^2 + 3u + 1) (p^4 - p^2 + 1) / r, a multiple of the hard exponent by a
+    factor coprime to r -- the same equality decisions; tests pin the device's GT bytes to this"""
+    t = f12_mul(f12_conj(f), f12_inv(f))
+    t = f12_mul(f12_frob(t, 2), t)
+    a = f12_exp_by_neg_u(t)
+    b = f12_sqr(a)
+    c = f12_sqr(b)
+    d = f12_mul(c, b)
+    e = f12_exp_by_neg_u(d)
+    f_ = f12_sqr(e)
+    g = f12_exp_by_neg_u(f_)
+    h = f12_conj(d)
+    i = f12_conj(g)
+    j = f12_mul(i, e)
+    k = f12_mul(j, h)
+    l_ = f12_mul(k, b)
+    m = f12_mul(k, e)
+    n = f12_mul(t, m)
+    o = f12_frob(l_, 1)
+    p_ = f12_mul(o, n)
+    q = f12_frob(k, 2)
+    r_ = f12_mul(q, p_)
+    s = f12_conj(t)
+    t2 = f12_mul(s, l_)
+    u_ = f12_frob(t2, 3)
+    return f12_mul(u_, r_)
+
+
+def gt_ints(f):
+    """the device's GT layout: w^0.c0, w^0.c1, ..., w^5.c1"""
+    return [x for c in f for x in c]

@@ -107,6 +107,12 @@ extern "C" {
                           value_balance: *const i64, bvk: *mut u8, status: *mut u8) -> c_int;
     pub fn zg_jubjub_decode(ctx: *mut ZgCtx, n: usize, points: *const u8, status: *mut u8, xy: *mut u8) -> c_int;
 
+    pub fn zg_pghr13_vk_load_builtin(ctx: *mut ZgCtx) -> c_int;
+    pub fn zg_pghr13_vk_load_json(ctx: *mut ZgCtx, json: *const c_char, len: usize) -> c_int;
+    pub fn zg_pghr13_verify(ctx: *mut ZgCtx, n: usize, proofs: *const u8, inputs: *const u8, n_inputs: *const u8,
+                            status: *mut u8, kernel_ms: *mut f32) -> c_int;
+    pub fn zg_bn254_pairing(ctx: *mut ZgCtx, n: usize, g1: *const u8, g2: *const u8, gt: *mut u8) -> c_int;
+
     pub fn zg_merkle_combine(ctx: *mut ZgCtx, kind: c_int, n: usize, left: *const u8, right: *const u8,
                              depth: *const u8, out: *mut u8) -> c_int;
     pub fn zg_tree_empty_roots(ctx: *mut ZgCtx, kind: c_int, levels: usize, out: *mut u8) -> c_int;

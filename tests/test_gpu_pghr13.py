@@ -1,0 +1,95 @@
+"""GPU parity of PGHR13 on BN254 against the oracle: the device pairing's
+GT bytes equal oracle.bn254's (Miller loop + the same final-exponentiation chain), every case of
+tests/golden/pghr13.json (the reference's vectors, mainnet block 522, mutants) gets the oracle's
+status, a mixed batch of 1,024, and the verifying-key checks."""
+import json
+import os
+import random
+
+import pytest
+
+from oracle import bn254 as B
+from tests.conftest import ROOT, load_golden
+
+GOLDEN = load_golden("pghr13.json")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zebra_amd import Context
+    c = Context(device=0, max_batch=64, load_builtin=False, seed=7)
+    yield c
+    c.close()
+
+
+def _inputs(case):
+    return [bytes.fromhex(x) for x in case["inputs"]]
+
+
+@pytest.mark.gpu
+def test_gpu_bn254_pairing_bytes(ctx):
+    rnd = random.Random(2)
+    ps = [B.G1_GEN, B.ec_mul(B._F1, B.G1_GEN, rnd.randrange(1, B.R))]
+    qs = [B.G2_GEN, B.ec_mul(B._F2, B.G2_GEN, rnd.randrange(1, B.R))]
+    got = ctx.bn254_pairing(ps, qs)
+    for p, q, g in zip(ps, qs, got):
+        assert g == B.gt_ints(B.final_exponentiation_fc(B.miller_loop([(p, q)])))
+    # bilinearity on the device alone
+    e1, e6 = ctx.bn254_pairing([B.G1_GEN, B.ec_mul(B._F1, B.G1_GEN, 6)], [B.ec_mul(B._F2, B.G2_GEN, 7), B.ec_mul(B._F2, B.G2_GEN, 7)])
+    assert e1 != e6
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_fixtures(ctx):
+    cases = GOLDEN["cases"]
+    got = ctx.pghr13_verify([bytes.fromhex(c["proof"]) for c in cases], [_inputs(c) for c in cases])
+    assert got == [c["status"] for c in cases], [(c["name"], g, c["status"]) for c, g in zip(cases, got)
+                                                  if g != c["status"]]
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_mixed_batch(ctx):
+    """1,024 proofs cycling through every fixture case (valid mainnet proofs and mutants)"""
+    cases = GOLDEN["cases"]
+    rnd = random.Random(4)
+    pick = [rnd.randrange(len(cases)) for _ in range(1024)]
+    got = ctx.pghr13_verify([bytes.fromhex(cases[k]["proof"]) for k in pick], [_inputs(cases[k]) for k in pick])
+    assert got == [cases[k]["status"] for k in pick]
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_inputs(ctx):
+    from zebra_amd import zg
+    c = next(c for c in GOLDEN["cases"] if c["name"] == "smoky_pghr")
+    ins = _inputs(c)
+    big = list(ins)
+    big[2] = B.R.to_bytes(32, "little")
+    got = ctx.pghr13_verify([bytes.fromhex(c["proof"])] * 3, [ins, big, ins[:8]])
+    assert got == [zg.STATUS_OK, zg.STATUS_INPUT_NONCANONICAL, zg.STATUS_VERIFY_FAILED]
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_vk_checks(ctx):
+    from zebra_amd import zg
+    d = json.load(open(os.path.join(ROOT, "zebra_amd", "res", "sprout-verifying-key.json")))
+    bad = dict(d)
+    bad["alphaB"] = [d["alphaB"][0], d["alphaB"][0]]      # off the curve
+    with pytest.raises(zg.ZgError) as ei:
+        ctx.pghr13_vk_load_json(json.dumps(bad))
+    assert ei.value.code == -4
+    # a twist point outside the order-r subgroup (AffineG2::new's order check)
+    x0 = 1
+    while True:
+        xx = (x0, 1)
+        y = B.f2_sqrt(B.f2_add(B.f2_mul(B.f2_sqr(xx), xx), B.B2))
+        if y is not None and B.ec_mul(B._F2, (xx, y), B.R) is not None:
+            break
+        x0 += 1
+    bad = dict(d)
+    bad["zeta"] = ["0x%064x" % xx[1], "0x%064x" % xx[0], "0x%064x" % y[1], "0x%064x" % y[0]]
+    with pytest.raises(zg.ZgError) as ei:
+        ctx.pghr13_vk_load_json(json.dumps(bad))
+    assert ei.value.code == -4
+    ctx.pghr13_vk_load_json(json.dumps(d))
+    c = GOLDEN["cases"][0]
+    assert ctx.pghr13_verify([bytes.fromhex(c["proof"])], [_inputs(c)]) == [c["status"]]

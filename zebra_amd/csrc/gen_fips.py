@@ -31,7 +31,7 @@ def column(prods, tag):
     n = len(prods)
     for k, (x, y) in enumerate(prods):
         c = "%[c0]" if k % 2 == 0 else "%[c1]"
-        text.append("v_mad_u64_u32 %%[lm], %s, %s, %s, %%[lm]" % (c, op(x, "v"), op(y, "s" if y.startswith(("FQ_P", "FR_R")) else "v")))
+        text.append("v_mad_u64_u32 %%[lm], %s, %s, %s, %%[lm]" % (c, op(x, "v"), op(y, "s" if y.startswith(("FQ_P", "FR_R", "BQ_P")) else "v")))
         if k >= 1:
             cp = "%[c0]" if (k - 1) % 2 == 0 else "%[c1]"
             text.append("v_addc_co_u32 %%[h], vcc, 0, %%[h], %s" % cp)
@@ -218,6 +218,9 @@ def main():
     out.append("")
     # Fr (the Jubjub base field): a, b < r < 2^255, so a b < 2^256 r and t < 2r < 2^256
     out += gen_mul("fr_mul_fips", 8, "FR_R", "FR_INV", "2^-256", "a, b < r", "< 2r < 2^256")
+    out.append("")
+    # BN254 Fq (PGHR13): a, b < p < 2^254
+    out += gen_mul("bq_mul_fips", 8, "BQ_P", "BQ_INV", "2^-256", "a, b < p", "< 2p < 2^255")
     out.append("")
     # ---- lazy-reduction building blocks: the 24-limb product and the Montgomery reduction of a
     # 24-limb value, the same column statements split in two (an Fq2 Karatsuba product reduces

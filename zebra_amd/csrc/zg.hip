@@ -43,6 +43,16 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
                       size_t n, const void* leaves, int leaves_on_device, size_t nmarks, const uint64_t* marks,
                       uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms,
                       void** arena, size_t* arena_cap, std::string* err);
+// zg_pghr13.hip
+struct BnDev;
+BnDev* bn_dev_new();
+void bn_dev_free(BnDev* d);
+int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, std::string* err);
+bool bn_vk_loaded(BnDev* d);
+int bn_pghr13_verify(BnDev* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
+                     const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
+                     std::string* err);
+int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt, std::string* err);
 }  // namespace zg
 
 // Per-device state shared by every context (batch slot) on that GPU: a FIXED pool of stream
@@ -71,6 +81,7 @@ struct zg_dev {
   std::vector<VKEntry*> vks;  // prepare_verifying_key once per distinct key per device
   uint32_t* jj_comb = nullptr;  // Jubjub generators' comb tables (zg_jubjub.h), built on first use
   zg::MerkleDev* merkle = nullptr;  // Pedersen table + empty roots (zg_merkle.hip), first use
+  zg::BnDev* bn = nullptr;          // PGHR13 key, line and comb tables (zg_pghr13.hip), first use
 };
 
 static std::mutex g_devs_mu;
@@ -174,6 +185,7 @@ static void dev_release(zg_dev* d) {
   }
   if (d->jj_comb) hipFree(d->jj_comb);
   merkle_dev_free(d->merkle);
+  bn_dev_free(d->bn);
   g_devs[d->device] = nullptr;
   delete d;
 }
@@ -1409,4 +1421,64 @@ extern "C" int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uin
                                     uint8_t* roots, uint8_t* state_out, size_t* state_out_len, float* kernel_ms) {
   return tree_roots(ctx, kind, height, state, state_len, n_leaves, d_leaves, 1, n_marks, marks, roots, state_out,
                     state_out_len, kernel_ms);
+}
+
+// ------------------------------------------------------------------ PGHR13 Sprout proofs (zg_pghr13.hip)
+static zg::BnDev* bn_dev(zg_ctx* ctx) {
+  zg_dev* d = ctx->dev;
+  std::lock_guard<std::mutex> g(d->mu);
+  if (!d->bn) d->bn = bn_dev_new();
+  return d->bn;
+}
+
+extern "C" int zg_pghr13_vk_load_json(zg_ctx* ctx, const char* json, size_t len) {
+  if (!ctx || !json) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return bn_load_vk_json(bn_dev(ctx), ctx->stream, json, len, &ctx->err);
+}
+
+extern "C" int zg_pghr13_vk_load_builtin(zg_ctx* ctx) {
+  return zg_pghr13_vk_load_json(ctx, ZG_PGHR13_VK_JSON, strlen(ZG_PGHR13_VK_JSON));
+}
+
+extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* inputs,
+                                const uint8_t* n_inputs, uint8_t* status, float* kernel_ms) {
+  if (!ctx || (n && (!proofs || !inputs || !status)) || n > (1u << 24)) return ZG_E_INVAL;
+  if (n_inputs)
+    for (size_t i = 0; i < n; i++)
+      if (n_inputs[i] > 9) return fail(ctx, ZG_E_INVAL, "at most 9 PGHR13 inputs per proof");
+  zg::BnDev* d = bn_dev(ctx);
+  if (!bn_vk_loaded(d)) {
+    int rc = zg_pghr13_vk_load_builtin(ctx);
+    if (rc) return rc;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!n) return ZG_OK;
+  // the equality weights rho_2..rho_5 (16 bytes each): seeded contexts (tests) derive them,
+  // others take them from the OS
+  std::vector<uint8_t> rho(64 * n);
+  if (ctx->seeded) {
+    for (size_t i = 0; i < n; i++) {
+      Blake2b h(64);
+      h.update("zg-pghr13-rho", 13);
+      uint8_t le[8];
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)(ctx->seed >> (8 * b));
+      h.update(le, 8);
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)((uint64_t)i >> (8 * b));
+      h.update(le, 8);
+      h.final(&rho[64 * i]);
+    }
+  } else if (!os_random(rho.data(), rho.size())) {
+    return fail(ctx, ZG_E_INVAL, "getrandom failed");
+  }
+  return bn_pghr13_verify(d, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status, kernel_ms, &ctx->err);
+}
+
+extern "C" int zg_bn254_pairing(zg_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt) {
+  if (!ctx || (n && (!g1 || !g2 || !gt)) || n > (1u << 20)) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  return bn_pairing(ctx->stream, n, g1, g2, gt, &ctx->err);
 }

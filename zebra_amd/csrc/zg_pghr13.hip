@@ -1,0 +1,659 @@
+// zg_pghr13.hip -- PGHR13 Sprout proofs on BN254: the kernels and the
+// host side of zg_pghr13_verify / zg_bn254_pairing.
+//
+// Reference: crypto/src/pghr13.rs:69-105 (Proof::from_raw, verify), called per PHGR JoinSplit by
+// verification/src/sprout.rs:61-67. verify checks five pairing equalities; here, per proof, the five
+// are folded into one product with random 128-bit weights rho_2..rho_5 (rho_1 = 1):
+//
+//   e(a, A) e(P1', P2) e(rho3 c, C) e(rho4 k, G) e(P5, GB2) e(P6, Z) e(P7, b) == 1
+//   P1' = -(a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   P7  = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a)
+//
+// which holds for all rho iff each equality holds (a false proof passes with probability
+// ~2^-128 over the rho, drawn from getrandom(2) per call). One multi-Miller loop over 7 pairs and
+// one final exponentiation per proof, instead of 10 pairings: the 6 verifying-key G2 points use
+// line tables built once per device, only the proof's b is doubled along the loop.
+//
+//   k_bn_vk       VK points -> Montgomery, AffineG1/G2::new checks (curve, G2 order r)
+//   k_bn_lines    line coefficients of the 6 fixed G2 points (lane per point)
+//   k_bn_comb     byte-window comb tables of the fixed G1 bases (ic[0..9], vk.b, gammaBeta1)
+//   k_pghr_prep   lane per proof: decode, acc = ic0 + sum x_i ic_{i+1}, the 7 G1 operands
+//   k_pghr_miller lane per proof: the multi-Miller loop -> f (HBM)
+//   k_fe_*        lane per proof: final exponentiation in 5 launches (HBM workspace), f == 1 -> status
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zg.h"
+#include "zg_bn254.h"
+
+namespace zg {
+
+#define ZG_BN_MAX_IC 16
+#define ZG_BN_FIXED_Q 6  // vk.a, P2 (G2::one), vk.c, vk.gamma, vk.gamma_beta_2, vk.z
+#define ZG_BN_NLINES 100  // >= 64 doublings + popcount of the low 64 bits of 6u+2 + 2
+#define ZG_BN_COMB_BASES (ZG_BN_MAX_IC + 2)
+#define ZG_BN_COMB_W 32
+#define ZG_BN_COMB_D 255
+#define ZG_BN_PTS 7
+
+struct BnVK {
+  BA2 q[ZG_BN_FIXED_Q];  // a, P2, c, gamma, gamma_beta_2, z
+  BA1 b, gb1;
+  BA1 ic[ZG_BN_MAX_IC];
+  int ic_len;
+  int err;  // 0 ok, 1 a point is not on its curve / not of order r
+};
+
+// canonical big-endian words (the host's JSON) -> Montgomery points, with the bn crate's checks
+__global__ void k_bn_vk(const uint32_t* raw, int ic_len, BnVK* vk) {
+  if (blockIdx.x | threadIdx.x) return;
+  // raw layout (each Fq 8 LE words, canonical): 5 G2 (x.c0, x.c1, y.c0, y.c1), b, gb1, ic[ic_len]
+  int err = 0;
+  auto fq = [&](int w) { return bq_to_mont(bq_c(raw + 8 * w)); };
+  for (int k = 0; k < 5; k++) {  // a, c, gamma, gb2, z into q[0], q[2..5]
+    BA2 q = {{fq(4 * k), fq(4 * k + 1)}, {fq(4 * k + 2), fq(4 * k + 3)}};
+    if (!ba2_on_curve(q) || !ba2_in_subgroup(q)) err = 1;
+    vk->q[k == 0 ? 0 : k + 1] = q;
+  }
+  vk->q[1] = {b2_c(BN_G2_X), b2_c(BN_G2_Y)};
+  int w = 20;
+  auto g1 = [&]() {
+    BA1 p = {fq(w), fq(w + 1), false};
+    w += 2;
+    if (!ba1_on_curve(p)) err = 1;
+    return p;
+  };
+  vk->b = g1();
+  vk->gb1 = g1();
+  for (int i = 0; i < ic_len; i++) vk->ic[i] = g1();
+  vk->ic_len = ic_len;
+  vk->err = err;
+}
+
+// the lines of fixed point j in Miller-loop order: per bit (top excluded) a doubling line, then
+// an addition line when the bit is set; then the pi(Q) and -pi^2(Q) lines
+__global__ void __launch_bounds__(64) k_bn_lines(const BnVK* vk, BLine* lines) {
+  const int j = threadIdx.x;
+  if (blockIdx.x || j >= ZG_BN_FIXED_Q) return;
+  const BA2 q = vk->q[j];
+  BH2 t = {q.x, q.y, b2_one()};
+  BLine* o = lines + (size_t)j * ZG_BN_NLINES;
+  int n = 0;
+  for (int i = ZG_BN_ATE_BITS - 2; i >= 0; i--) {
+    o[n++] = bh2_dbl_step(&t);
+    if (bn_ate_bit(i)) o[n++] = bh2_add_step(&t, q);
+  }
+  const BA2 q1 = ba2_frob(q), q2 = ba2_frob2(q);
+  o[n++] = bh2_add_step(&t, q1);
+  o[n++] = bh2_add_step(&t, {q2.x, b2_neg(q2.y)});
+}
+
+// comb tables: entry (base, w, d) = d 2^(8 w) base, affine Montgomery (x, y), 16 words
+__global__ void __launch_bounds__(64) k_bn_comb(const BnVK* vk, uint32_t* table) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D) return;
+  const int d = t % ZG_BN_COMB_D + 1, w = (t / ZG_BN_COMB_D) % ZG_BN_COMB_W, base = t / (ZG_BN_COMB_D * ZG_BN_COMB_W);
+  BA1 p = {bq_zero(), bq_zero(), true};
+  if (base < vk->ic_len)
+    p = vk->ic[base];
+  else if (base == ZG_BN_MAX_IC)
+    p = vk->b;
+  else if (base == ZG_BN_MAX_IC + 1)
+    p = vk->gb1;
+  uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int bit = 8 * w;
+  k[bit >> 5] = (uint32_t)d << (bit & 31);
+  const BA1 r = p.inf ? p : bj1_to_aff(bj1_mul(p, k, 256));
+  uint32_t* e = table + (size_t)t * 16;
+  for (int l = 0; l < 8; l++) {
+    e[l] = r.inf ? 0u : r.x.l[l];
+    e[8 + l] = r.inf ? 0u : r.y.l[l];
+  }
+}
+
+// [s] base_j from the comb table (s: nbytes little-endian bytes)
+ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s, int nbytes) {
+  for (int w = 0; w < nbytes; w++) {
+    const int d = s[w];
+    if (!d) continue;
+    const uint32_t* e = comb + ((size_t)(base * ZG_BN_COMB_W + w) * ZG_BN_COMB_D + (d - 1)) * 16;
+    BA1 p;
+    for (int l = 0; l < 8; l++) {
+      p.x.l[l] = e[l];
+      p.y.l[l] = e[8 + l];
+    }
+    p.inf = false;
+    acc = bj1_add_aff(acc, p);
+  }
+  return acc;
+}
+
+// G1::from_compressed (33 bytes)
+ZG_INL bool bn_g1_decode(const uint8_t* b, BA1* out) {
+  const uint8_t sign = b[0];
+  if (sign != 2 && sign != 3) return false;
+  Bq x;
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = b + 1 + 28 - 4 * i;
+    x.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  if (!fp_lt_modulus<BqM>(x)) return false;
+  const Bq xm = bq_to_mont(x);
+  const Bq three = bq_add(bq_dbl(bq_one()), bq_one());
+  Bq y;
+  if (!bq_sqrt(bq_add(bq_mul(bq_sqr(xm), xm), three), &y)) return false;
+  const bool odd = bq_from_mont(y).l[0] & 1u;
+  if ((sign == 2) == odd) y = bq_neg(y);
+  *out = {xm, y, false};
+  return true;
+}
+
+// G2::from_compressed (65 bytes): x from the 512-bit blob U = c1 p + c0 (long division), y by
+// the y_gt flag, then the order check
+ZG_INL bool bn_g2_decode(const uint8_t* b, BA2* out) {
+  const uint8_t sign = b[0];
+  if (sign != 10 && sign != 11) return false;
+  // U / p by shift-subtract over the 512 bits (MSB first); remainder < p < 2^254
+  uint32_t rem[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, quo[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool q_big = false;  // quotient >= 2^256 (then certainly >= p)
+  for (int i = 0; i < 512; i++) {
+    const uint32_t bit = (b[1 + (i >> 3)] >> (7 - (i & 7))) & 1u;
+#pragma unroll
+    for (int k = 8; k > 0; k--) rem[k] = (rem[k] << 1) | (rem[k - 1] >> 31);
+    rem[0] = (rem[0] << 1) | bit;
+    // rem >= p ?
+    uint32_t t[9];
+    uint64_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const uint64_t d = (uint64_t)rem[k] - (k < 8 ? BQ_P[k] : 0u) - br;
+      t[k] = (uint32_t)d;
+      br = (d >> 63) & 1u;
+    }
+    const bool ge = br == 0;
+    q_big |= (quo[7] >> 31) != 0;  // the quotient is about to exceed 256 bits
+#pragma unroll
+    for (int k = 7; k > 0; k--) quo[k] = (quo[k] << 1) | (quo[k - 1] >> 31);
+    quo[0] = (quo[0] << 1) | (ge ? 1u : 0u);
+#pragma unroll
+    for (int k = 0; k < 9; k++) rem[k] = ge ? t[k] : rem[k];
+  }
+  Bq c0, c1;
+  for (int k = 0; k < 8; k++) {
+    c0.l[k] = rem[k];
+    c1.l[k] = quo[k];
+  }
+  if (q_big || !fp_lt_modulus<BqM>(c1)) return false;  // Fq2::from_slice: c1 must be < p
+  BA2 q;
+  q.x = {bq_to_mont(c0), bq_to_mont(c1)};
+  Bq2 y;
+  if (!b2_sqrt(b2_add(b2_mul(b2_sqr(q.x), q.x), b2_c(BQ_B2)), &y)) return false;
+  // y_gt: y > -y in the order c1 p + c0 (compare c1, then c0, canonical)
+  const Bq2 yn = b2_neg(y);
+  const Bq y0 = bq_from_mont(y.c0), y1 = bq_from_mont(y.c1), n0 = bq_from_mont(yn.c0), n1 = bq_from_mont(yn.c1);
+  const bool gt = bq_eq(y1, n1) ? fp_gt_canon<BqM>(y0, n0) : fp_gt_canon<BqM>(y1, n1);
+  if ((sign == 10) == gt) y = yn;
+  q.y = y;
+  if (!ba2_in_subgroup(q)) return false;
+  *out = q;
+  return true;
+}
+
+struct PghrPts {  // per proof, written by k_pghr_prep
+  BA1 p[ZG_BN_PTS];
+  BA2 qb;
+};
+
+__global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* proofs, const uint8_t* inputs,
+                                                   const uint8_t* ninputs, const uint8_t* rho, const BnVK* vk,
+                                                   const uint32_t* comb, PghrPts* pts, uint8_t* status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* pr = proofs + (size_t)296 * i;
+  BA1 a, ap, bp, c, cp, k, h;
+  BA2 qb;
+  const bool ok = bn_g1_decode(pr, &a) && bn_g1_decode(pr + 33, &ap) && bn_g2_decode(pr + 66, &qb) &&
+                  bn_g1_decode(pr + 131, &bp) && bn_g1_decode(pr + 164, &c) && bn_g1_decode(pr + 197, &cp) &&
+                  bn_g1_decode(pr + 230, &k) && bn_g1_decode(pr + 263, &h);
+  if (!ok) {
+    status[i] = ZG_STATUS_DECODE_INVALID;
+    return;
+  }
+  // acc = ic0 + sum x_j ic_{j+1} over min(count, ic_len - 1) inputs (the reference's zip)
+  int cnt = ninputs ? ninputs[i] : 9;
+  cnt = cnt < vk->ic_len - 1 ? cnt : vk->ic_len - 1;
+  const uint8_t* xin = inputs + (size_t)9 * 32 * i;
+  BJ1 acc = bj1_from(vk->ic[0]);
+  for (int j = 0; j < cnt; j++) {
+    Bq x;
+    for (int l = 0; l < 8; l++)
+      x.l[l] = (uint32_t)xin[32 * j + 4 * l] | ((uint32_t)xin[32 * j + 4 * l + 1] << 8) |
+               ((uint32_t)xin[32 * j + 4 * l + 2] << 16) | ((uint32_t)xin[32 * j + 4 * l + 3] << 24);
+    bool lt_r = false;  // x < r (bn::Fr)
+    {
+      uint64_t br = 0;
+      for (int l = 0; l < 8; l++) {
+        const uint64_t d = (uint64_t)x.l[l] - BN_R[l] - br;
+        br = (d >> 63) & 1u;
+      }
+      lt_r = br != 0;
+    }
+    if (!lt_r) {
+      status[i] = ZG_STATUS_INPUT_NONCANONICAL;
+      return;
+    }
+    acc = bn_comb_mul(acc, comb, j + 1, xin + 32 * j, 32);
+  }
+  const BA1 acca = bj1_to_aff(acc);
+  const uint8_t* r = rho + (size_t)64 * i;  // rho2, rho3, rho4, rho5: 16 LE bytes each
+  uint32_t rw[4][4];
+  for (int q = 0; q < 4; q++)
+    for (int l = 0; l < 4; l++)
+      rw[q][l] = (uint32_t)r[16 * q + 4 * l] | ((uint32_t)r[16 * q + 4 * l + 1] << 8) |
+                 ((uint32_t)r[16 * q + 4 * l + 2] << 16) | ((uint32_t)r[16 * q + 4 * l + 3] << 24);
+  const BA1 aa = ba1_add(acca, a);      // acc + a
+  const BA1 aac = ba1_add(aa, c);       // acc + a + c
+  PghrPts& o = pts[i];
+  o.p[0] = a;
+  // P1' = -(a' + rho2 b' + rho3 c' + rho5 c)
+  BJ1 s = bj1_from(ap);
+  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(bp, rw[0], 128)));
+  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(cp, rw[1], 128)));
+  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(c, rw[3], 128)));
+  o.p[1] = ba1_neg(bj1_to_aff(s));
+  o.p[2] = bj1_to_aff(bj1_mul(c, rw[1], 128));
+  o.p[3] = bj1_to_aff(bj1_mul(k, rw[2], 128));
+  o.p[4] = aac.inf ? aac : ba1_neg(bj1_to_aff(bj1_mul(aac, rw[2], 128)));
+  o.p[5] = ba1_neg(bj1_to_aff(bj1_mul(h, rw[3], 128)));
+  // P7 = rho2 vk.b - rho4 gb1 + rho5 (acc + a)
+  BJ1 t = bj1_inf();
+  t = bn_comb_mul(t, comb, ZG_BN_MAX_IC, r, 16);
+  const BA1 g4 = bj1_to_aff(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 16));
+  t = bj1_add_aff(t, ba1_neg(g4));
+  if (!aa.inf) t = bj1_add_aff(t, bj1_to_aff(bj1_mul(aa, rw[3], 128)));
+  o.p[6] = bj1_to_aff(t);
+  o.qb = qb;
+  status[i] = ZG_STATUS_OK;
+}
+
+// the multi-Miller loop of one proof's 7 pairs -> f
+__global__ void __launch_bounds__(64) k_pghr_miller(int n, const PghrPts* pts, const BLine* lines,
+                                                     const uint8_t* status, Bq12* fout) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  const PghrPts& P = pts[i];
+  const BA2 qb = P.qb;
+  BH2 t = {qb.x, qb.y, b2_one()};
+  Bq12 f = b12_one();
+  int li = 0;
+  for (int bit = ZG_BN_ATE_BITS - 2; bit >= -2; bit--) {
+    // bit >= 0: a doubling step (+ an addition when set); -1, -2: the pi(Q), -pi^2(Q) additions
+    const int nsub = bit >= 0 ? (bn_ate_bit(bit) ? 2 : 1) : 1;
+    if (bit >= 0) f = b12_sqr(f);
+    for (int s = 0; s < nsub; s++, li++) {
+      for (int j = 0; j < ZG_BN_FIXED_Q; j++) {
+        const BA1 p = P.p[j];
+        if (p.inf) continue;
+        f = b12_mul_bline(f, lines[(size_t)j * ZG_BN_NLINES + li], p);
+      }
+      BLine l;
+      if (bit >= 0)
+        l = s == 0 ? bh2_dbl_step(&t) : bh2_add_step(&t, qb);
+      else if (bit == -1)
+        l = bh2_add_step(&t, ba2_frob(qb));
+      else {
+        const BA2 q2 = ba2_frob2(qb);
+        l = bh2_add_step(&t, {q2.x, b2_neg(q2.y)});
+      }
+      if (!P.p[6].inf) f = b12_mul_bline(f, l, P.p[6]);
+    }
+  }
+  fout[i] = f;
+}
+
+// the final exponentiation of zg_bn254.h bn_final_exp, split so that no kernel holds more than
+// a few Fq12 values at once (a lane-per-proof Fq12 is 96 VGPRs): the chain's intermediates live in
+// a per-proof HBM workspace w[0..5] = t, b, d, e, g, (spare)
+#define ZG_FE_SLOTS 6
+__global__ void __launch_bounds__(64) k_fe_easy(int n, const Bq12* f, const uint8_t* status, Bq12* w) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  const Bq12 x = f[i];
+  const Bq12 t = b12_mul(b12_conj(x), b12_inv(x));
+  w[(size_t)ZG_FE_SLOTS * i + 0] = b12_mul(b12_frob(t, 2), t);
+}
+// stage 1: a = t^-u, b = a^2, d = b^3 ; stage 2: e = d^-u ; stage 3: g = (e^2)^-u
+template <int STAGE>
+__global__ void __launch_bounds__(64) k_fe_exp(int n, const uint8_t* status, Bq12* w) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  Bq12* s = w + (size_t)ZG_FE_SLOTS * i;
+  if (STAGE == 1) {
+    const Bq12 b = b12_sqr(b12_exp_by_neg_u(s[0]));
+    s[1] = b;
+    s[2] = b12_mul(b12_sqr(b), b);
+  } else if (STAGE == 2) {
+    s[3] = b12_exp_by_neg_u(s[2]);
+  } else {
+    s[4] = b12_exp_by_neg_u(b12_sqr(s[3]));
+  }
+}
+// k = g^-1 e d^-1, l = k b, n = t k e ; result = (t^-1 l)^(p^3) k^(p^2) l^p n == 1 ?
+__global__ void __launch_bounds__(64) k_fe_last(int n, uint8_t* status, Bq12* w) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  Bq12* s = w + (size_t)ZG_FE_SLOTS * i;
+  const Bq12 k = b12_mul(b12_mul(b12_conj(s[4]), s[3]), b12_conj(s[2]));
+  s[5] = k;
+  const Bq12 l = b12_mul(k, s[1]);
+  s[4] = l;  // g is dead
+  Bq12 r = b12_mul(s[0], b12_mul(k, s[3]));           // n
+  r = b12_mul(b12_frob(l, 1), r);                      // p
+  r = b12_mul(b12_frob(s[5], 2), r);                   // r
+  r = b12_mul(b12_frob(b12_mul(b12_conj(s[0]), s[4]), 3), r);
+  status[i] = b12_is_one(r) ? ZG_STATUS_OK : ZG_STATUS_VERIFY_FAILED;
+}
+
+// zg_bn254_pairing (tests): the Miller loop of e(P, Q) -> f; the final exponentiation then runs
+// through the k_fe_* kernels above and k_bn_gt writes GT as 12 canonical LE Fq in the order
+// w^0.c0, w^0.c1, w^1.c0, ..., w^5.c1 (oracle.bn254.gt_ints)
+__global__ void __launch_bounds__(64) k_bn_miller1(int n, const uint32_t* g1, const uint32_t* g2, Bq12* fout) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* a = g1 + 16 * (size_t)i;
+  const uint32_t* q = g2 + 32 * (size_t)i;
+  const BA1 p = {bq_to_mont(bq_c(a)), bq_to_mont(bq_c(a + 8)), false};
+  const BA2 Q = {{bq_to_mont(bq_c(q)), bq_to_mont(bq_c(q + 8))}, {bq_to_mont(bq_c(q + 16)), bq_to_mont(bq_c(q + 24))}};
+  BH2 t = {Q.x, Q.y, b2_one()};
+  Bq12 f = b12_one();
+  for (int bit = ZG_BN_ATE_BITS - 2; bit >= 0; bit--) {
+    f = b12_sqr(f);
+    f = b12_mul_bline(f, bh2_dbl_step(&t), p);
+    if (bn_ate_bit(bit)) f = b12_mul_bline(f, bh2_add_step(&t, Q), p);
+  }
+  f = b12_mul_bline(f, bh2_add_step(&t, ba2_frob(Q)), p);
+  const BA2 q2 = ba2_frob2(Q);
+  fout[i] = b12_mul_bline(f, bh2_add_step(&t, {q2.x, b2_neg(q2.y)}), p);
+}
+// the full exponent's last stage (k_fe_last without the comparison)
+__global__ void __launch_bounds__(64) k_bn_gt(int n, Bq12* w, uint32_t* gt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Bq12* s = w + (size_t)ZG_FE_SLOTS * i;
+  const Bq12 k = b12_mul(b12_mul(b12_conj(s[4]), s[3]), b12_conj(s[2]));
+  s[5] = k;
+  const Bq12 l = b12_mul(k, s[1]);
+  s[4] = l;
+  Bq12 r = b12_mul(s[0], b12_mul(k, s[3]));
+  r = b12_mul(b12_frob(l, 1), r);
+  r = b12_mul(b12_frob(s[5], 2), r);
+  r = b12_mul(b12_frob(b12_mul(b12_conj(s[0]), s[4]), 3), r);
+  const Bq2 cs[6] = {r.c0.c0, r.c1.c0, r.c0.c1, r.c1.c1, r.c0.c2, r.c1.c2};  // w^0 .. w^5
+  uint32_t* o = gt + 96 * (size_t)i;
+  for (int k2 = 0; k2 < 6; k2++) {
+    const Bq x0 = bq_from_mont(cs[k2].c0), x1 = bq_from_mont(cs[k2].c1);
+    for (int l2 = 0; l2 < 8; l2++) {
+      o[16 * k2 + l2] = x0.l[l2];
+      o[16 * k2 + 8 + l2] = x1.l[l2];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side
+struct BnDev {
+  std::mutex mu;
+  BnVK* vk = nullptr;
+  BLine* lines = nullptr;
+  uint32_t* comb = nullptr;
+  int err = 0;  // the loaded key failed AffineG*::new
+};
+
+BnDev* bn_dev_new() { return new BnDev(); }
+void bn_dev_free(BnDev* d) {
+  if (!d) return;
+  if (d->vk) hipFree(d->vk);
+  if (d->lines) hipFree(d->lines);
+  if (d->comb) hipFree(d->comb);
+  delete d;
+}
+
+#define BCHK(expr)                                            \
+  do {                                                        \
+    hipError_t e_ = (expr);                                   \
+    if (e_ != hipSuccess) {                                   \
+      *err = std::string(#expr ": ") + hipGetErrorString(e_); \
+      return ZG_E_HIP;                                        \
+    }                                                         \
+  } while (0)
+
+static unsigned bn_blocks(long long n) { return (unsigned)((n + 63) / 64); }
+
+// hex strings of the key's JSON members in document order (crypto/src/json/pghr13.rs layout)
+static bool json_hex_list(const std::string& js, const char* key, std::vector<std::string>* out) {
+  const std::string k = std::string("\"") + key + "\"";
+  size_t pos = js.find(k);
+  if (pos == std::string::npos) return false;
+  pos = js.find('[', pos);
+  if (pos == std::string::npos) return false;
+  int depth = 0;
+  for (size_t i = pos; i < js.size(); i++) {
+    const char ch = js[i];
+    if (ch == '[') depth++;
+    if (ch == ']' && --depth == 0) return true;
+    if (ch == '"') {
+      const size_t e = js.find('"', i + 1);
+      if (e == std::string::npos) return false;
+      std::string s = js.substr(i + 1, e - i - 1);
+      if (s.rfind("0x", 0) == 0) s = s.substr(2);
+      out->push_back(s);
+      i = e;
+    }
+  }
+  return false;
+}
+
+// a big-endian hex Fq (Fq::from_slice: at most 32 bytes, < p) -> 8 LE words
+static bool hex_fq(const std::string& h, uint32_t* w) {
+  if (h.size() > 64 || h.empty()) return false;
+  uint8_t b[32] = {0};
+  const std::string s = std::string(64 - h.size(), '0') + h;
+  for (int i = 0; i < 32; i++) {
+    unsigned v;
+    if (sscanf(s.c_str() + 2 * i, "%2x", &v) != 1) return false;
+    b[i] = (uint8_t)v;
+  }
+  for (int l = 0; l < 8; l++) {
+    const uint8_t* q = b + 28 - 4 * l;
+    w[l] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  for (int l = 7; l >= 0; l--)
+    if (w[l] != BQ_P[l]) return w[l] < BQ_P[l];
+  return false;
+}
+
+int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, std::string* err) {
+  std::lock_guard<std::mutex> g(d->mu);
+  const std::string js(json, len);
+  std::vector<uint32_t> raw;
+  auto put = [&](const std::string& h) {
+    uint32_t w[8];
+    if (!hex_fq(h, w)) return false;
+    raw.insert(raw.end(), w, w + 8);
+    return true;
+  };
+  // G2 [x_a, x_b, y_a, y_b] -> x = (x_b, x_a), y = (y_b, y_a)
+  for (const char* k : {"alphaA", "alphaC", "gamma", "gammaBeta2", "zeta"}) {
+    std::vector<std::string> v;
+    if (!json_hex_list(js, k, &v) || v.size() != 4) {
+      *err = std::string("PGHR13 key: bad member ") + k;
+      return ZG_E_VK;
+    }
+    if (!put(v[1]) || !put(v[0]) || !put(v[3]) || !put(v[2])) {
+      *err = std::string("PGHR13 key: field element of ") + k;
+      return ZG_E_VK;
+    }
+  }
+  for (const char* k : {"alphaB", "gammaBeta1"}) {
+    std::vector<std::string> v;
+    if (!json_hex_list(js, k, &v) || v.size() != 2 || !put(v[0]) || !put(v[1])) {
+      *err = std::string("PGHR13 key: bad member ") + k;
+      return ZG_E_VK;
+    }
+  }
+  std::vector<std::string> ic;
+  if (!json_hex_list(js, "ic", &ic) || ic.size() % 2 || ic.size() < 2 || ic.size() / 2 > ZG_BN_MAX_IC) {
+    *err = "PGHR13 key: bad ic";
+    return ZG_E_VK;
+  }
+  for (const auto& h : ic)
+    if (!put(h)) {
+      *err = "PGHR13 key: ic field element";
+      return ZG_E_VK;
+    }
+  const int ic_len = (int)ic.size() / 2;
+  if (!d->vk) {
+    BCHK(hipMalloc(&d->vk, sizeof(BnVK)));
+    BCHK(hipMalloc(&d->lines, sizeof(BLine) * ZG_BN_FIXED_Q * ZG_BN_NLINES));
+    BCHK(hipMalloc(&d->comb, (size_t)ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D * 64));
+  }
+  uint32_t* draw;
+  BCHK(hipMalloc(&draw, raw.size() * 4));
+  hipError_t e = hipMemcpyAsync(draw, raw.data(), raw.size() * 4, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_bn_vk, dim3(1), dim3(64), 0, st, draw, ic_len, d->vk);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_bn_lines, dim3(1), dim3(64), 0, st, d->vk, d->lines);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_bn_comb, dim3(bn_blocks(ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D)), dim3(64), 0, st,
+                       d->vk, d->comb);
+    e = hipGetLastError();
+  }
+  int verr = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&verr, &d->vk->err, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(draw);
+  if (e != hipSuccess) {
+    *err = std::string("PGHR13 key upload: ") + hipGetErrorString(e);
+    return ZG_E_HIP;
+  }
+  d->err = verr;
+  if (verr) {
+    *err = "PGHR13 key: a point is not on its curve or not of order r (AffineG*::new)";
+    return ZG_E_VK;
+  }
+  return ZG_OK;
+}
+
+bool bn_vk_loaded(BnDev* d) { return d->vk && !d->err; }
+
+int bn_pghr13_verify(BnDev* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
+                     const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
+                     std::string* err) {
+  if (!n) return ZG_OK;
+  // device buffers of this call
+  struct Bufs {
+    std::vector<void*> p;
+    ~Bufs() {
+      for (void* q : p) hipFree(q);
+    }
+  } bufs;
+  auto alloc = [&](void** x, size_t b) {
+    hipError_t e = hipMalloc(x, b ? b : 1);
+    if (e == hipSuccess) bufs.p.push_back(*x);
+    return e;
+  };
+  uint8_t *dp, *din, *dni = nullptr, *drho, *dst;
+  PghrPts* dpts;
+  Bq12* df;
+  BCHK(alloc((void**)&dp, 296 * n));
+  BCHK(alloc((void**)&din, 9 * 32 * n));
+  BCHK(alloc((void**)&drho, 64 * n));
+  BCHK(alloc((void**)&dst, n));
+  BCHK(alloc((void**)&dpts, sizeof(PghrPts) * n));
+  BCHK(alloc((void**)&df, sizeof(Bq12) * n));
+  Bq12* dw;
+  BCHK(alloc((void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n));
+  BCHK(hipMemcpyAsync(dp, proofs, 296 * n, hipMemcpyHostToDevice, st));
+  BCHK(hipMemcpyAsync(din, inputs, 9 * 32 * n, hipMemcpyHostToDevice, st));
+  BCHK(hipMemcpyAsync(drho, rho, 64 * n, hipMemcpyHostToDevice, st));
+  if (ninputs) {
+    BCHK(alloc((void**)&dni, n));
+    BCHK(hipMemcpyAsync(dni, ninputs, n, hipMemcpyHostToDevice, st));
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (kernel_ms) {
+    BCHK(hipEventCreate(&e0));
+    BCHK(hipEventCreate(&e1));
+    BCHK(hipEventRecord(e0, st));
+  }
+  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, din, dni, drho, d->vk, d->comb,
+                     dpts, dst);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dpts, d->lines, dst, df);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_exp<1>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_exp<2>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_exp<3>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_last, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+  BCHK(hipGetLastError());
+  if (kernel_ms) BCHK(hipEventRecord(e1, st));
+  BCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, st));
+  BCHK(hipStreamSynchronize(st));
+  if (kernel_ms) {
+    BCHK(hipEventElapsedTime(kernel_ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  return ZG_OK;
+}
+
+int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt, std::string* err) {
+  if (!n) return ZG_OK;
+  uint32_t *a = nullptr, *b = nullptr, *o = nullptr;
+  Bq12 *f = nullptr, *w = nullptr;
+  uint8_t* ok = nullptr;
+  hipError_t e = hipMalloc(&a, 64 * n);
+  if (e == hipSuccess) e = hipMalloc(&b, 128 * n);
+  if (e == hipSuccess) e = hipMalloc(&o, 384 * n);
+  if (e == hipSuccess) e = hipMalloc(&f, sizeof(Bq12) * n);
+  if (e == hipSuccess) e = hipMalloc(&w, sizeof(Bq12) * ZG_FE_SLOTS * n);
+  if (e == hipSuccess) e = hipMalloc(&ok, n);
+  if (e == hipSuccess) e = hipMemsetAsync(ok, ZG_STATUS_OK, n, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(a, g1, 64 * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(b, g2, 128 * n, hipMemcpyHostToDevice, st);
+  const unsigned nb = bn_blocks(n);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_bn_miller1, dim3(nb), dim3(64), 0, st, (int)n, a, b, f);
+    hipLaunchKernelGGL(k_fe_easy, dim3(nb), dim3(64), 0, st, (int)n, f, ok, w);
+    hipLaunchKernelGGL(k_fe_exp<1>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);
+    hipLaunchKernelGGL(k_fe_exp<2>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);
+    hipLaunchKernelGGL(k_fe_exp<3>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);
+    hipLaunchKernelGGL(k_bn_gt, dim3(nb), dim3(64), 0, st, (int)n, w, o);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(gt, o, 384 * n, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  for (void* q : {(void*)a, (void*)b, (void*)o, (void*)f, (void*)w, (void*)ok})
+    if (q) hipFree(q);
+  if (e != hipSuccess) {
+    *err = std::string("zg_bn254_pairing: ") + hipGetErrorString(e);
+    return ZG_E_HIP;
+  }
+  return ZG_OK;
+}
+
+}  // namespace zg

@@ -71,6 +71,10 @@ def lib():
                                      ctypes.POINTER(ctypes.c_int64), u8p, u8p]
         L.zg_jubjub_decode.argtypes = [vp, sz, u8p, u8p, u8p]
         L.zg_merkle_combine.argtypes = [vp, i, sz, u8p, u8p, u8p, u8p]
+        L.zg_pghr13_vk_load_builtin.argtypes = [vp]
+        L.zg_pghr13_vk_load_json.argtypes = [vp, u8p, sz]
+        L.zg_pghr13_verify.argtypes = [vp, sz, u8p, u8p, u8p, u8p, ctypes.POINTER(ctypes.c_float)]
+        L.zg_bn254_pairing.argtypes = [vp, sz, u8p, u8p, u8p]
         L.zg_tree_empty_roots.argtypes = [vp, i, sz, u8p]
         L.zg_tree_state_max_bytes.restype = sz
         L.zg_tree_state_max_bytes.argtypes = [i]
@@ -308,6 +312,39 @@ class Context:
         self._chk(lib().zg_jubjub_decode(self._p, n, b"".join(map(bytes, points)), st, xy))
         return [(st.raw[i], int.from_bytes(xy.raw[64 * i:64 * i + 32], "little"),
                  int.from_bytes(xy.raw[64 * i + 32:64 * i + 64], "little")) for i in range(n)]
+
+    # ---- PGHR13 Sprout proofs on BN254 (include/zg.h zg_pghr13_* / zg_bn254_pairing)
+    def pghr13_vk_load_json(self, text):
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        self._chk(lib().zg_pghr13_vk_load_json(self._p, b, len(b)))
+
+    def pghr13_verify(self, proofs, inputs, n_inputs=None, with_time=False):
+        """proofs: 296-byte PHGR proofs; inputs: per proof a list of <= 9 32-byte LE BN254 Fr
+        (Input::into_bn_frs) -> statuses (STATUS_*)"""
+        n = len(proofs)
+        rows = []
+        for r in inputs:
+            r = [bytes(x) for x in r]
+            assert len(r) <= 9
+            rows.append(b"".join(r) + bytes(32 * (9 - len(r))))
+        cnt = bytes(len(r) for r in inputs) if n_inputs is None else bytes(n_inputs)
+        st = ctypes.create_string_buffer(max(n, 1))
+        ms = ctypes.c_float(0)
+        self._chk(lib().zg_pghr13_verify(self._p, n, b"".join(map(bytes, proofs)), b"".join(rows), cnt, st,
+                                         ctypes.byref(ms)))
+        out = list(st.raw[:n])
+        return (out, ms.value) if with_time else out
+
+    def bn254_pairing(self, g1s, g2s):
+        """device pairing (tests): g1 (x, y) ints, g2 ((x0, x1), (y0, y1)) -> 12 ints per GT"""
+        n = len(g1s)
+        a = b"".join(x.to_bytes(32, "little") + y.to_bytes(32, "little") for x, y in g1s)
+        b = b"".join(q[0][0].to_bytes(32, "little") + q[0][1].to_bytes(32, "little") +
+                     q[1][0].to_bytes(32, "little") + q[1][1].to_bytes(32, "little") for q in g2s)
+        out = ctypes.create_string_buffer(max(384 * n, 1))
+        self._chk(lib().zg_bn254_pairing(self._p, n, a, b, out))
+        return [[int.from_bytes(out.raw[384 * i + 32 * k:384 * i + 32 * k + 32], "little") for k in range(12)]
+                for i in range(n)]
 
     # ---- note-commitment trees (include/zg.h zg_merkle_combine / zg_tree_*)
     def merkle_combine(self, kind, lefts, rights, depths=None):
