@@ -35,7 +35,13 @@ namespace zg {
 
 #define ZG_BN_MAX_IC 16
 #define ZG_BN_FIXED_Q 6  // vk.a, P2 (G2::one), vk.c, vk.gamma, vk.gamma_beta_2, vk.z
-#define ZG_BN_NLINES 100  // >= 64 doublings + popcount of the low 64 bits of 6u+2 + 2
+#define ZG_BN_NLINES 102  // 64 doublings + 36 additions (popcount of the low 64 bits of 6u + 2) + 2
+constexpr int bn_lines_needed() {
+  int n = 2;  // the pi(Q), -pi^2(Q) steps
+  for (int i = ZG_BN_ATE_BITS - 2; i >= 0; i--) n += 1 + (int)((BN_ATE[i >> 5] >> (i & 31)) & 1u);
+  return n;
+}
+static_assert(bn_lines_needed() <= ZG_BN_NLINES, "line table rows");
 #define ZG_BN_COMB_BASES (ZG_BN_MAX_IC + 2)
 #define ZG_BN_COMB_W 32
 #define ZG_BN_COMB_D 255
