@@ -433,6 +433,15 @@ def main():
                 trees[name]["cpu_baseline"] = bench_tree.cpu_window(kind, h, 64, 4.0)
                 trees[name]["gpu_over_cpu"] = trees[name]["leaves_per_s"] / trees[name]["cpu_baseline"]["leaves_per_s"]
         out["note_commitment_trees"] = trees
+        # PGHR13 Sprout proofs on BN254 (tools/bench_pghr13.py), not the headline
+        from tools import bench_pghr13
+        pg = bench_pghr13.run(ctx, 65536, 2)
+        pg["workload"] = ("65,536 PHGR JoinSplit proofs cycling through the 9 valid reference / block-522 "
+                          "statements; host buffers (zg_pghr13_verify)")
+        if not args.no_cpu:
+            pg["cpu_baseline"] = bench_pghr13.cpu_baseline(4.0)
+            pg["gpu_over_cpu"] = pg["proofs_per_s"] / pg["cpu_baseline"]["proofs_per_s"]
+        out["pghr13_sprout_proofs"] = pg
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(proofs, kinds, inputs, args.cpu_seconds, cpu_threads(args.cpu_threads))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
