@@ -11,6 +11,8 @@ nproc > $O/host.txt; grep -m1 "model name" /proc/cpuinfo >> $O/host.txt; echo "O
 if [ -z "$2" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
   tail -3 $O/gpu_tests.log
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
 fi
 t0=$(date +%s.%N)
 timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
@@ -22,4 +24,6 @@ python3 -c "import json; d=json.load(open('$O/bench_8192_if8.json')); print('819
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof_bench_iso.json 2> $O/prof_bench_iso.err || { echo "rocprof iso failed"; tail -30 $O/prof_bench_iso.err; exit 1; }
-cd $R && python3 tools/rocpd_stats.py $O/prof/run_results.db $O/kernel_stats.csv && python3 tools/rocpd_stats.py $O/prof_iso/run_results.db $O/kernel_stats_isolated.csv
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_tree -o run -- python3 $R/tools/bench_tree.py --no-cpu --reps 5 > $O/prof_tree.json 2> $O/prof_tree.err || { echo "rocprof trees failed"; tail -30 $O/prof_tree.err; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_pghr -o run -- python3 $R/tools/bench_pghr13.py --no-cpu --reps 2 > $O/prof_pghr.json 2> $O/prof_pghr.err || { echo "rocprof pghr13 failed"; tail -30 $O/prof_pghr.err; exit 1; }
+cd $R && for k in prof prof_iso prof_tree prof_pghr; do python3 tools/rocpd_stats.py $O/$k/run_results.db $O/kernel_stats_${k#prof}.csv; done
