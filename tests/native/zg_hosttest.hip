@@ -5,6 +5,7 @@
 #include "../../zebra_amd/csrc/zg_coop.h"
 #include "../../zebra_amd/csrc/zg_groth16.h"
 #include "../../zebra_amd/csrc/zg_bingcd.h"
+#include "../../zebra_amd/csrc/zg_bn254.h"
 
 using namespace zg;
 
@@ -38,6 +39,42 @@ void zgt_fr_inv_vt_mont(const uint8_t* a, uint8_t* out) {
   memcpy(out, r.l, 32);
 }
 void zgt_fq_inv_vt(const uint8_t* a, uint8_t* out) { fq_limbs_to_be(fp_inv_vt<FqM, ZG_INV_T_FQ>(fq_limbs_from_be(a)), out); }
+// BN254 (PGHR13): the device's codecs and pairing on the CPU; points canonical LE
+static void st_bq(const Bq& a, uint8_t* o) {
+  const Bq c = bq_from_mont(a);
+  memcpy(o, c.l, 32);
+}
+static Bq ld_bq(const uint8_t* b) {
+  Bq x;
+  memcpy(x.l, b, 32);
+  return bq_to_mont(x);
+}
+int zgt_bn_g1_decode(const uint8_t* in, uint8_t* out) {
+  BA1 p;
+  if (!bn_g1_decode(in, &p)) return 0;
+  st_bq(p.x, out);
+  st_bq(p.y, out + 32);
+  return 1;
+}
+int zgt_bn_g2_decode(const uint8_t* in, uint8_t* out) {
+  BA2 q;
+  if (!bn_g2_decode(in, &q)) return 0;
+  st_bq(q.x.c0, out);
+  st_bq(q.x.c1, out + 32);
+  st_bq(q.y.c0, out + 64);
+  st_bq(q.y.c1, out + 96);
+  return 1;
+}
+void zgt_bn_pairing(const uint8_t* g1, const uint8_t* g2, uint8_t* gt) {
+  const BA1 p = {ld_bq(g1), ld_bq(g1 + 32), false};
+  const BA2 q = {{ld_bq(g2), ld_bq(g2 + 32)}, {ld_bq(g2 + 64), ld_bq(g2 + 96)}};
+  const Bq12 f = bn_final_exp(bn_miller_single(p, q));
+  const Bq2 cs[6] = {f.c0.c0, f.c1.c0, f.c0.c1, f.c1.c1, f.c0.c2, f.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    st_bq(cs[k].c0, gt + 64 * k);
+    st_bq(cs[k].c1, gt + 64 * k + 32);
+  }
+}
 void zgt_f12_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   f12_to_bytes(f12_mul(f12_from_bytes(a), f12_from_bytes(b)), out);
 }

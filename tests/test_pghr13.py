@@ -55,3 +55,45 @@ def test_fixture_shape():
     real = [n for n in st if n.startswith(("verification", "smoky", "h522"))]
     assert len(real) == 9 and all(st[n] == PG.OK for n in real)
     assert {st[n] for n in st if n.startswith("mut_")} == {PG.INVALID_ENCODING, PG.INVALID_PROOF}
+
+
+# ---- the product's BN254 code (zg_bn254.h) on the CPU (tests/native host harness)
+def _host():
+    from tests import hostlib
+    return hostlib.lib(), hostlib.buf
+
+
+def test_host_bn254_decoders_match_oracle():
+    """every point of every fixture proof through the device decoders compiled for the host:
+    same accept / reject and the same coordinates as the oracle (bn crate codecs)"""
+    L, buf = _host()
+    out = buf(128)
+    for c in GOLDEN["cases"]:
+        raw = bytes.fromhex(c["proof"])
+        for off, ln in ((0, 33), (33, 33), (66, 65), (131, 33), (164, 33), (197, 33), (230, 33), (263, 33)):
+            enc = raw[off:off + ln]
+            try:
+                want = B.g1_from_compressed(enc) if ln == 33 else B.g2_from_compressed(enc)
+            except B.DecodeError:
+                want = None
+            ok = (L.zgt_bn_g1_decode if ln == 33 else L.zgt_bn_g2_decode)(enc, out)
+            assert bool(ok) == (want is not None), (c["name"], off)
+            if ok and ln == 33:
+                assert (int.from_bytes(out.raw[:32], "little"), int.from_bytes(out.raw[32:64], "little")) == want
+            elif ok:
+                v = [int.from_bytes(out.raw[32 * k:32 * k + 32], "little") for k in range(4)]
+                assert ((v[0], v[1]), (v[2], v[3])) == want
+
+
+def test_host_bn254_pairing_matches_oracle():
+    import random
+    L, buf = _host()
+    rnd = random.Random(3)
+    p = B.ec_mul(B._F1, B.G1_GEN, rnd.randrange(1, B.R))
+    q = B.ec_mul(B._F2, B.G2_GEN, rnd.randrange(1, B.R))
+    g1 = p[0].to_bytes(32, "little") + p[1].to_bytes(32, "little")
+    g2 = b"".join(v.to_bytes(32, "little") for v in (q[0][0], q[0][1], q[1][0], q[1][1]))
+    out = buf(384)
+    L.zgt_bn_pairing(g1, g2, out)
+    got = [int.from_bytes(out.raw[32 * k:32 * k + 32], "little") for k in range(12)]
+    assert got == B.gt_ints(B.final_exponentiation_fc(B.miller_loop([(p, q)])))

@@ -139,77 +139,6 @@ ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s
   return acc;
 }
 
-// G1::from_compressed (33 bytes)
-ZG_INL bool bn_g1_decode(const uint8_t* b, BA1* out) {
-  const uint8_t sign = b[0];
-  if (sign != 2 && sign != 3) return false;
-  Bq x;
-  for (int i = 0; i < 8; i++) {
-    const uint8_t* q = b + 1 + 28 - 4 * i;
-    x.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-  }
-  if (!fp_lt_modulus<BqM>(x)) return false;
-  const Bq xm = bq_to_mont(x);
-  const Bq three = bq_add(bq_dbl(bq_one()), bq_one());
-  Bq y;
-  if (!bq_sqrt(bq_add(bq_mul(bq_sqr(xm), xm), three), &y)) return false;
-  const bool odd = bq_from_mont(y).l[0] & 1u;
-  if ((sign == 2) == odd) y = bq_neg(y);
-  *out = {xm, y, false};
-  return true;
-}
-
-// G2::from_compressed (65 bytes): x from the 512-bit blob U = c1 p + c0 (long division), y by
-// the y_gt flag, then the order check
-ZG_INL bool bn_g2_decode(const uint8_t* b, BA2* out) {
-  const uint8_t sign = b[0];
-  if (sign != 10 && sign != 11) return false;
-  // U / p by shift-subtract over the 512 bits (MSB first); remainder < p < 2^254
-  uint32_t rem[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, quo[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  bool q_big = false;  // quotient >= 2^256 (then certainly >= p)
-  for (int i = 0; i < 512; i++) {
-    const uint32_t bit = (b[1 + (i >> 3)] >> (7 - (i & 7))) & 1u;
-#pragma unroll
-    for (int k = 8; k > 0; k--) rem[k] = (rem[k] << 1) | (rem[k - 1] >> 31);
-    rem[0] = (rem[0] << 1) | bit;
-    // rem >= p ?
-    uint32_t t[9];
-    uint64_t br = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const uint64_t d = (uint64_t)rem[k] - (k < 8 ? BQ_P[k] : 0u) - br;
-      t[k] = (uint32_t)d;
-      br = (d >> 63) & 1u;
-    }
-    const bool ge = br == 0;
-    q_big |= (quo[7] >> 31) != 0;  // the quotient is about to exceed 256 bits
-#pragma unroll
-    for (int k = 7; k > 0; k--) quo[k] = (quo[k] << 1) | (quo[k - 1] >> 31);
-    quo[0] = (quo[0] << 1) | (ge ? 1u : 0u);
-#pragma unroll
-    for (int k = 0; k < 9; k++) rem[k] = ge ? t[k] : rem[k];
-  }
-  Bq c0, c1;
-  for (int k = 0; k < 8; k++) {
-    c0.l[k] = rem[k];
-    c1.l[k] = quo[k];
-  }
-  if (q_big || !fp_lt_modulus<BqM>(c1)) return false;  // Fq2::from_slice: c1 must be < p
-  BA2 q;
-  q.x = {bq_to_mont(c0), bq_to_mont(c1)};
-  Bq2 y;
-  if (!b2_sqrt(b2_add(b2_mul(b2_sqr(q.x), q.x), b2_c(BQ_B2)), &y)) return false;
-  // y_gt: y > -y in the order c1 p + c0 (compare c1, then c0, canonical)
-  const Bq2 yn = b2_neg(y);
-  const Bq y0 = bq_from_mont(y.c0), y1 = bq_from_mont(y.c1), n0 = bq_from_mont(yn.c0), n1 = bq_from_mont(yn.c1);
-  const bool gt = bq_eq(y1, n1) ? fp_gt_canon<BqM>(y0, n0) : fp_gt_canon<BqM>(y1, n1);
-  if ((sign == 10) == gt) y = yn;
-  q.y = y;
-  if (!ba2_in_subgroup(q)) return false;
-  *out = q;
-  return true;
-}
-
 struct PghrPts {  // per proof, written by k_pghr_prep
   BA1 p[ZG_BN_PTS];
   BA2 qb;
@@ -375,16 +304,7 @@ __global__ void __launch_bounds__(64) k_bn_miller1(int n, const uint32_t* g1, co
   const uint32_t* q = g2 + 32 * (size_t)i;
   const BA1 p = {bq_to_mont(bq_c(a)), bq_to_mont(bq_c(a + 8)), false};
   const BA2 Q = {{bq_to_mont(bq_c(q)), bq_to_mont(bq_c(q + 8))}, {bq_to_mont(bq_c(q + 16)), bq_to_mont(bq_c(q + 24))}};
-  BH2 t = {Q.x, Q.y, b2_one()};
-  Bq12 f = b12_one();
-  for (int bit = ZG_BN_ATE_BITS - 2; bit >= 0; bit--) {
-    f = b12_sqr(f);
-    f = b12_mul_bline(f, bh2_dbl_step(&t), p);
-    if (bn_ate_bit(bit)) f = b12_mul_bline(f, bh2_add_step(&t, Q), p);
-  }
-  f = b12_mul_bline(f, bh2_add_step(&t, ba2_frob(Q)), p);
-  const BA2 q2 = ba2_frob2(Q);
-  fout[i] = b12_mul_bline(f, bh2_add_step(&t, {q2.x, b2_neg(q2.y)}), p);
+  fout[i] = bn_miller_single(p, Q);
 }
 // the full exponent's last stage (k_fe_last without the comparison)
 __global__ void __launch_bounds__(64) k_bn_gt(int n, Bq12* w, uint32_t* gt) {
