@@ -9,6 +9,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -82,6 +83,7 @@ struct zg_dev {
   uint32_t* jj_comb = nullptr;  // Jubjub generators' comb tables (zg_jubjub.h), built on first use
   zg::MerkleDev* merkle = nullptr;  // Pedersen table + empty roots (zg_merkle.hip), first use
   zg::BnDev* bn = nullptr;          // PGHR13 key, line and comb tables (zg_pghr13.hip), first use
+  std::atomic<int> inflight{0};     // contexts on this device with a batch begun and not finished
 };
 
 static std::mutex g_devs_mu;
@@ -300,6 +302,8 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   return ctx;
 }
 
+static void set_state(zg_ctx* ctx, int st);
+
 extern "C" void zg_destroy(zg_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
@@ -315,6 +319,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
     if (ctx->ev[i]) hipEventDestroy(ctx->ev[i]);
+  set_state(ctx, 0);
   zg_dev* d = ctx->dev;
   delete ctx;
   if (d) dev_release(d);
@@ -696,8 +701,12 @@ static int run_pipeline(zg_ctx* ctx) {
   // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
   const unsigned pgroups = (unsigned)((ctx->npad / 2 + 63) / 64);
+  // auto: fuse only a lone batch whose two grids are resident at once. With other batches in
+  // flight on the device the split launches overlap them better (8k shards, 6 in flight: 3.79
+  // vs 4.20 ms/batch, profiles/r02i_sweep8k.txt), and a fused grid would share the CUs anyway.
   const bool fused = ctx->fuse == 1 ||
-                     (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu);
+                     (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu &&
+                      ctx->dev->inflight.load(std::memory_order_relaxed) == 0);
   ctx->fused_last = fused;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
@@ -745,6 +754,13 @@ static int check_kinds(zg_ctx* ctx, size_t n, const uint8_t* kinds) {
   return ZG_OK;
 }
 
+// ctx->state 0 <-> 1 transitions keep the device's in-flight count (the auto fusion policy)
+static void set_state(zg_ctx* ctx, int st) {
+  if (ctx->state == st) return;
+  if (ctx->dev) ctx->dev->inflight.fetch_add(st ? 1 : -1, std::memory_order_relaxed);
+  ctx->state = st;
+}
+
 static int begin_common(zg_ctx* ctx, size_t n) {
   if (ctx->state != 0) return fail(ctx, ZG_E_STATE, "zg_batch_begin with a batch in flight (finish it first)");
   if (n > ctx->cap) return fail(ctx, ZG_E_NOMEM, "batch larger than max_batch");
@@ -777,7 +793,7 @@ static int batch_begin_locked(zg_ctx* ctx, size_t n, const uint8_t* proofs, cons
   }
   ctx->cur_ninputs = n_inputs ? ctx->d_ninputs : nullptr;
   if ((rc = run_pipeline(ctx))) return rc;
-  ctx->state = 1;
+  set_state(ctx, 1);
   return ZG_OK;
 }
 
@@ -813,7 +829,7 @@ extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs
   }
   ctx->cur_ninputs = d_n_inputs ? ctx->d_ninputs : nullptr;
   if ((rc = run_pipeline(ctx))) return rc;
-  ctx->state = 1;
+  set_state(ctx, 1);
   return ZG_OK;
 }
 
@@ -1031,12 +1047,12 @@ static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool 
   if (!batch_ok) {
     int rc = bisect(ctx, st, root_failed);
     if (rc) {
-      ctx->state = 0;  // the batch is abandoned; the context stays usable
+      set_state(ctx, 0);  // the batch is abandoned; the context stays usable
       return rc;
     }
   }
   for (size_t i = 0; i < ctx->n; i++) status[i] = st[i] == ST_PENDING ? ST_OK : st[i];
-  ctx->state = 0;
+  set_state(ctx, 0);
   return ZG_OK;
 }
 
@@ -1058,7 +1074,7 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
   if (!rc) rc = check_nodes(ctx, root, 0, &okv, nullptr);
   if (!rc) rc = collect_batch_stats(ctx);
   if (rc) {
-    ctx->state = 0;
+    set_state(ctx, 0);
     return rc;
   }
   return batch_finish_locked(ctx, okv[0], status, /*root_failed=*/okv[0] == 0);
