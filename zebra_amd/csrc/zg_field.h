@@ -20,6 +20,13 @@
 #define ZG_INL __host__ __device__ __forceinline__
 #define ZG_NOINL __host__ __device__ __attribute__((noinline))
 
+// ZG_FQ29 (default): Fq products in 29-bit digits (zg_fq29.h / gen_fq29.py); 0: the 32-bit-word
+// FIPS asm (zg_fips.h) on the device
+#ifndef ZG_FQ29
+#define ZG_FQ29 1
+#endif
+#include "zg_fq29_gen.h"
+
 namespace zg {
 
 struct FqM {
@@ -231,7 +238,9 @@ ZG_NOINL inline u32x16 fq_mul_v(u32x8 a0, u32x4 a1, u32x8 b0, u32x4 b1) {
     b.l[8 + i] = b1[i];
   }
   Fq r;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if ZG_FQ29
+  fq29_mul(r.l, a.l, b.l);     // 29-bit digits, carry-free v_mad_u64_u32 columns (host: same code)
+#elif defined(__HIP_DEVICE_COMPILE__)
   fq_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning
 #else
   r = fp_mul_inl<FqM>(a, b);   // host build of the test harness (tests/native): portable CIOS
@@ -293,7 +302,37 @@ ZG_INL Fr fr_mul(const Fr& a, const Fr& b) {
   return r;
 }
 
+#if ZG_FQ29
+ZG_NOINL inline u32x16 fq_sqr_v(u32x8 a0, u32x4 a1) {
+  Fq a;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a.l[i] = a0[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) a.l[8 + i] = a1[i];
+  Fq r;
+  fq29_sqr(r.l, a.l);  // 105 + 196 digit products (a < 2p)
+  u32x16 o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o[i] = r.l[i];
+  o[12] = o[13] = o[14] = o[15] = 0;
+  return o;
+}
+ZG_INL Fq fq_sqr(const Fq& a) {
+  u32x8 a0;
+  u32x4 a1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a0[i] = a.l[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) a1[i] = a.l[8 + i];
+  u32x16 o = fq_sqr_v(a0, a1);
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = o[i];
+  return r;
+}
+#else
 ZG_INL Fq fq_sqr(const Fq& a) { return fq_mul(a, a); }
+#endif
 ZG_INL Fq fq_add(const Fq& a, const Fq& b) { return fp_add<FqM>(a, b); }
 ZG_INL Fq fq_sub(const Fq& a, const Fq& b) { return fp_sub<FqM>(a, b); }
 ZG_INL Fq fq_neg(const Fq& a) { return fp_neg<FqM>(a); }
