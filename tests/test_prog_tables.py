@@ -36,8 +36,15 @@ def run(name, inputs):
 def test_prog_schedule_structure():
     for name, prog, outs, nw, sch in gen_prog.build_all():
         assert all(len(r) <= nw for r in sch["rounds"])
-        # a slot is never written in the round that reads its previous content
+        # LDS: one f-chain block per CU; two R-chain blocks per CU (13 slots x 6 KB each)
         assert sch["nslots"] * 6 * 1024 <= 160 * 1024, name
+        if name in ("dbl", "add"):
+            assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
+            # B and C (outputs 4, 5) leave through their products' waves: no slot
+            assert sorted(sch["sinks"].values()) == [4, 5], name
+        else:
+            # no read barrier: a slot is never written in the round that reads its previous content
+            assert sch["rb"] == 0, name
 
 
 def test_line_programs_match_pairing_steps():

@@ -60,11 +60,13 @@ class G(dict):
 
 
 class Prog:
-    def __init__(self, name, inputs, keep=()):
+    def __init__(self, name, inputs, keep=(), glob=None):
         self.name = name
         self.inputs = list(inputs)
         self.keep = set(keep)  # inputs whose slots must survive the program
+        self.glob = dict(glob or {})  # input -> index of a per-lane global-memory operand (no LDS slot)
         self.prods = []        # (L, R, kind)
+        self.sink_from = None  # outputs >= this index may be stored by their product's wave
 
     def inp(self, i):
         return G({("in", i): (1, 0)})
@@ -91,6 +93,7 @@ def prog_dbl():
     """pairing doubling_step + ell scaling. in: X Y Z PQ (PQ = (px, py)). out: X' Y' Z' and
     the scaled line A + B v + C v w with A = c2, B = c1 px, C = c0 py"""
     p = Prog("dbl", ["X", "Y", "Z", "PQ"], keep=[3])
+    p.sink_from = 3
     X, Y, Z, PQ = (p.inp(i) for i in range(4))
     tmp0 = p.sqr(X)
     tmp1 = p.sqr(Y)
@@ -115,7 +118,9 @@ def prog_dbl():
 
 def prog_add():
     """pairing addition_step + ell scaling. in: X Y Z PQ QX QY."""
-    p = Prog("add", ["X", "Y", "Z", "PQ", "QX", "QY"], keep=[3])
+    # QX, QY (the proof's B) are read from HBM where an operand needs them: two LDS slots fewer
+    p = Prog("add", ["X", "Y", "Z", "PQ", "QX", "QY"], keep=[3], glob={4: 0, 5: 1})
+    p.sink_from = 3
     X, Y, Z, PQ, QX, QY = (p.inp(i) for i in range(6))
     zsq = p.sqr(Z)
     ysq = p.sqr(QY)
@@ -224,25 +229,88 @@ def prog_mm():
 
 
 # ---------------------------------------------------------------- scheduling + slots
-def schedule(prog, outs, nw, search=0, max_slots=None):
+# Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
+# Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
+# operand formation ~4.4 per instruction of its mod-p add / sub chains (37 per Fq op).
+PROD_CLK = {K_MUL: 8600, K_SQR: 6500, K_MULC0: 6500, K_MULC1: 6500}
+
+
+def _form_instr(f, lazy):
+    terms = list(f.values())
+    if len(terms) == 1 and terms[0] == (1, 0):
+        return 0
+    if lazy and len(terms) == 2 and all(t == (1, 0) for t in terms):
+        return 24
+    n = 0
+    for c0, c1 in terms:
+        if (c0, c1) in ((1, 0), (-1, 0)):
+            pass
+        elif (c0, c1) in ((1, 1), (-1, -1)) or c1 == 0 and abs(c0) == 2:
+            n += 74
+        elif (c0, c1) in ((0, 1), (0, -1)):
+            n += 25
+        else:
+            n += 74 * 3
+    return n + 74 * (len(terms) - 1)
+
+
+def prod_costs(prog):
+    out = []
+    for L, R, kind in prog.prods:
+        c = _form_instr(L, True) + (0 if kind == K_SQR else _form_instr(R, False))
+        out.append(PROD_CLK[kind] + 4.4 * c)
+    return out
+
+
+def balance_rounds(sch, costs, nw):
+    """order each round's products over the waves so that the two waves of a SIMD (w, w + nw/2)
+    carry a heavy and a light product; returns the modelled time (sum over rounds of the
+    busiest SIMD's load)"""
+    half = nw // 2
+    total = 0
+    for r, pick in enumerate(sch["rounds"]):
+        srt = sorted(pick, key=lambda i: -costs[i])
+        srt += [None] * (nw - len(srt))
+        order = [None] * nw
+        for sidx in range(half):  # heaviest with lightest
+            order[sidx], order[sidx + half] = srt[sidx], srt[nw - 1 - sidx]
+        c = lambda i: 0 if i is None else costs[i]
+        total += max(c(order[k]) + c(order[k + half]) for k in range(half))
+        sch["rounds"][r] = order  # None: an idle wave
+    return total
+
+
+def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, cost=False):
     """list-schedule products into rounds of <= nw; allocate LDS slots with reuse.
     search > 0: also try that many seeded random tie-breaks among ready products and keep the
-    schedule with the fewest rounds whose slots fit max_slots (then the fewest slots)."""
-    best = _schedule(prog, outs, nw, None, 0)
+    schedule with the fewest rounds whose slots fit max_slots (then the fewest slots).
+    shift 0: a slot may be rewritten in the round of its last read (the engine then puts a
+    barrier between a round's operand reads and its writes: ProgInfo.rb). partial: the random
+    candidates may also take fewer than nw ready products in a round (shorter live ranges)."""
+    best = _schedule(prog, outs, nw, None, 0, shift)
+    if cost:
+        costs = prod_costs(prog)
+        best["time"] = balance_rounds(best, costs, nw)
     if search:
         rng = random.Random(20260101)
         for t in range(search):
-            cand = _schedule(prog, outs, nw, rng, rng.choice([0.5, 1.5, 3, 6]))
+            slacks = [0.5, 1.5, 3, 6, 12] if partial else [0.5, 1.5, 3, 6]
+            cand = _schedule(prog, outs, nw, rng, rng.choice(slacks), shift, partial)
             fits = max_slots is None or cand["nslots"] <= max_slots
             bfits = max_slots is None or best["nslots"] <= max_slots
-            key = (not fits, len(cand["rounds"]), cand["nslots"])
-            bkey = (not bfits, len(best["rounds"]), best["nslots"])
+            if cost:  # modelled time (SIMD-balanced rounds) instead of the round count
+                cand["time"] = balance_rounds(cand, costs, nw)
+                key = (not fits, cand["time"], cand["nslots"])
+                bkey = (not bfits, best["time"], best["nslots"])
+            else:
+                key = (not fits, len(cand["rounds"]), cand["nslots"])
+                bkey = (not bfits, len(best["rounds"]), best["nslots"])
             if key < bkey:
                 best = cand
     return best
 
 
-def _schedule(prog, outs, nw, rng, slack):
+def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False):
     n = len(prog.prods)
     deps = []
     for L, R, _ in prog.prods:
@@ -254,13 +322,26 @@ def _schedule(prog, outs, nw, rng, slack):
     height = [0] * n
     for i in reversed(range(n)):
         height[i] = 1 + max([height[j] for j in succ[i]] or [0])
+    # sinks: products whose only use is to be output j >= sink_from as they stand (a line
+    # coefficient that goes to HBM): the wave stores them there and they take no LDS slot
+    sinks = {}
+    if prog.sink_from is not None:
+        used = {k[1] for L, R, _ in prog.prods for k in list(L) + list(R) if k[0] == "p"}
+        for j, f in enumerate(outs):
+            if j >= prog.sink_from and len(f) == 1:
+                (k, c), = f.items()
+                if k[0] == "p" and c == (1, 0) and k[1] not in used and k[1] not in sinks:
+                    sinks[k[1]] = j
     rnd = [None] * n
     rounds = []
     done = set()
     while len(done) < n:
         ready = [i for i in range(n) if rnd[i] is None and all(j in done for j in deps[i])]
         ready.sort(key=lambda i: (-height[i] + (rng.random() * slack if rng else 0), i))
-        pick = ready[:nw]
+        take = nw
+        if partial and rng is not None and rng.random() < 0.3:
+            take = rng.randrange(1, nw + 1)
+        pick = ready[:take]
         for i in pick:
             rnd[i] = len(rounds)
         rounds.append(pick)
@@ -271,18 +352,25 @@ def _schedule(prog, outs, nw, rng, slack):
     for i, (L, R, _) in enumerate(prog.prods):
         for k in list(L) + list(R):
             last[k] = max(last.get(k, -1), rnd[i])
-    for f in outs:
+    for j, f in enumerate(outs):
         for k in f:
-            last[k] = max(last.get(k, -1), nr)
+            if not (k[0] == "p" and sinks.get(k[1]) == j):
+                last[k] = max(last.get(k, -1), nr)
     nin = len(prog.inputs)
-    slot = {("in", i): i for i in range(nin)}
+    lds_in = [i for i in range(nin) if i not in prog.glob]
+    assert lds_in == list(range(len(lds_in))), "global-memory inputs come last"
+    slot = {("in", i): i for i in lds_in}
+    slot.update({("in", i): ("g", j) for i, j in prog.glob.items()})
     free_at = {}  # slot -> first round it may be rewritten
-    for i in range(nin):
+    for i in lds_in:
         if i not in prog.keep:
-            free_at[i] = last.get(("in", i), -1) + 1
-    nslots = nin
+            free_at[i] = last.get(("in", i), -1) + shift
+    nslots = len(lds_in)
     for r, pick in enumerate(rounds):
         for i in pick:
+            if i in sinks:
+                slot[("p", i)] = ("sink", sinks[i])
+                continue
             cand = sorted(s for s, fr in free_at.items() if fr <= r)
             if cand:
                 s = cand[0]
@@ -290,18 +378,18 @@ def _schedule(prog, outs, nw, rng, slack):
                 s = nslots
                 nslots += 1
             slot[("p", i)] = s
-            free_at[s] = last.get(("p", i), nr) + 1
+            free_at[s] = last.get(("p", i), nr) + shift
     # outputs are written to input slots 0.. after the output round: they must not clobber a
     # kept input
     assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add")
-    return {"rounds": rounds, "slot": slot, "nslots": nslots, "rnd": rnd}
+    return {"rounds": rounds, "slot": slot, "nslots": nslots, "rnd": rnd, "rb": int(shift == 0), "sinks": sinks}
 
 
 def simulate(prog, outs, sch, vals):
     """run the schedule on an LDS model with the slot map; returns output values"""
     lds = {}
     for i, v in enumerate(vals):
-        lds[i] = v
+        lds[sch["slot"][("in", i)]] = v
 
     def ev(f):
         r0 = r1 = 0
@@ -313,6 +401,8 @@ def simulate(prog, outs, sch, vals):
     for pick in sch["rounds"]:
         res = []
         for i in pick:
+            if i is None:
+                continue
             L, R, kind = prog.prods[i]
             x, y = ev(L), ev(R)
             if kind == K_MULC0:
@@ -320,9 +410,9 @@ def simulate(prog, outs, sch, vals):
             elif kind == K_MULC1:
                 y = (y[1], 0)
             res.append((i, ((x[0] * y[0] - x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)))
-        for i, v in res:  # all reads of a round precede its writes
+        for i, v in res:  # all reads of a round precede its writes (rb: enforced by a barrier)
             lds[sch["slot"][("p", i)]] = v
-    return [ev(f) for f in outs]
+    return [lds[("sink", j)] if j in sch["sinks"].values() else ev(f) for j, f in enumerate(outs)]
 
 
 def reference(prog, outs, vals):
@@ -348,7 +438,7 @@ def reference(prog, outs, vals):
 # ---------------------------------------------------------------- code generation
 def scaled(s, c0, c1):
     """(C++ expression, sign) of (c0 + c1 u) * atom-in-slot-s"""
-    x = "at.get(%d)" % s
+    x = "at.q(%d)" % s[1] if isinstance(s, tuple) else "at.get(%d)" % s
     if (c0, c1) in ((1, 0), (-1, 0)):
         return x, c0
     if (c0, c1) in ((1, 1), (-1, -1)):
@@ -363,9 +453,10 @@ def scaled(s, c0, c1):
 def form_code(f, slot, lazy):
     """C++ expression for a form. lazy: the value feeds a product as its lazy operand, so a
     plain sum / difference of two canonical atoms may skip the reduction (< 2p)."""
-    terms = [scaled(slot[k], c0, c1) for k, (c0, c1) in sorted(f.items(), key=lambda kv: slot[kv[0]])]
+    order = lambda kv: (1, slot[kv[0]][1]) if isinstance(slot[kv[0]], tuple) else (0, slot[kv[0]])
+    terms = [scaled(slot[k], c0, c1) for k, (c0, c1) in sorted(f.items(), key=order)]
     terms.sort(key=lambda t: -t[1])  # a positive term first
-    if lazy and len(terms) == 2 and all(t[0].startswith("at.get") for t in terms) and terms[0][1] > 0:
+    if lazy and len(terms) == 2 and all(t[0].startswith(("at.get", "at.q")) for t in terms) and terms[0][1] > 0:
         return "f2_lz_%s(%s, %s)" % ("add" if terms[1][1] > 0 else "sub", terms[0][0], terms[1][0])
     e, sg = terms[0]
     acc = e if sg > 0 else "f2_neg(%s)" % e
@@ -396,25 +487,36 @@ def emit(specs):
                     x, y = lx, form_code(R, s, False)
                 else:
                     x, y = form_code(R, s, True), form_code(L, s, False)
-            prod_cases.append("  case %d: x = %s; y = %s; dst = %d; return %d;  // %s p%d round %d" % (
-                gk + i, x, y, s[("p", i)], kind, name, i, sch["rnd"][i]))
+            d = s[("p", i)]
+            dst = SINK_BASE + d[1] if isinstance(d, tuple) else d
+            prod_cases.append("  case %d: x = %s; y = %s; dst = %d; return %d;  // %s p%d round %d%s" % (
+                gk + i, x, y, dst, kind, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else ""))
         for j, f in enumerate(outs):
-            out_cases.append("  case %d: return %s;  // %s out %d" % (go + j, form_code(f, sch["slot"], False),
-                                                                    name, j))
+            if j in sch.get("sinks", {}).values():
+                out_cases.append("  case %d: return f2_zero();  // %s out %d: stored by its product" % (go + j, name, j))
+            else:
+                out_cases.append("  case %d: return %s;  // %s out %d" % (go + j, form_code(f, sch["slot"], False),
+                                                                        name, j))
         off = len(sched)
         for pick in sch["rounds"]:
-            sched.extend(pick + [-1] * (nw - len(pick)))
-        infos.append((name, nin, len(prog.prods), len(outs), len(sch["rounds"]), nw, off, gk, go, sch["nslots"]))
+            sched.extend([-1 if i is None else i for i in pick] + [-1] * (nw - len(pick)))
+        infos.append((name, nin, len(prog.prods), len(outs), len(sch["rounds"]), nw, off, gk, go, sch["nslots"],
+                      sch["rb"]))
         gk += len(prog.prods)
         go += len(outs)
-    out.append("struct ProgInfo { int nin, nprod, nout, nrounds, nw, sched, gk, go, nslots; };")
-    for k, (name, nin, npr, nout, nr, nw, off, g1, g2, ns) in enumerate(infos):
-        out.append("#define ZG_PROG_%s %d  // %d products in %d rounds of %d waves, %d LDS slots" % (
-            name.upper(), k, npr, nr, nw, ns))
+    out.append("struct ProgInfo { int nin, nprod, nout, nrounds, nw, sched, gk, go, nslots, rb; };")
+    for k, (name, nin, npr, nout, nr, nw, off, g1, g2, ns, rb) in enumerate(infos):
+        out.append("#define ZG_PROG_%s %d  // %d products in %d rounds of %d waves, %d LDS slots%s" % (
+            name.upper(), k, npr, nr, nw, ns, ", read barrier" if rb else ""))
     out.append("__device__ __constant__ const ProgInfo PROG_INFO[%d] = {%s};" % (len(infos), ", ".join(
-        "{%d, %d, %d, %d, %d, %d, %d, %d, %d}" % i[1:] for i in infos)))
+        "{%d, %d, %d, %d, %d, %d, %d, %d, %d, %d}" % i[1:] for i in infos)))
     out.append("__device__ __constant__ const int8_t PROG_SCHED[%d] = {%s};" % (len(sched), ", ".join(
         map(str, sched))))
+    lsinks = [sorted(sch.get("sinks", {}).values()) for name, prog, outs, nw, sch in specs if name in ("dbl", "add")]
+    assert all(x == lsinks[0] for x in lsinks), lsinks
+    out.append("#define ZG_SINK_BASE %d  // dst >= this: the product is output (dst - base), stored to HBM" % SINK_BASE)
+    out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
+               sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
                          ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
@@ -435,8 +537,10 @@ def emit(specs):
     return out
 
 
-NW_LINES = 6
+SINK_BASE = 64
+NW_LINES = 4   # one wave per SIMD; 13 slots (78 KB) so that two blocks share a CU
 NW_FCHAIN = 8
+LINES_MAX_SLOTS = 13
 
 
 def build_all():
@@ -445,7 +549,13 @@ def build_all():
                    (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
-        sch = schedule(prog, outs, nw, 3000, 25) if fn in (prog_mmsq, prog_mm) else schedule(prog, outs, nw)
+        if fn in (prog_mmsq, prog_mm):
+            sch = schedule(prog, outs, nw, 3000, 25)
+        elif fn in (prog_dbl, prog_add):
+            sch = schedule(prog, outs, nw, 6000, LINES_MAX_SLOTS, shift=0, partial=True)
+            assert sch["nslots"] <= LINES_MAX_SLOTS, (prog.name, sch["nslots"])
+        else:
+            sch = schedule(prog, outs, nw)
         specs.append((prog.name, prog, outs, nw, sch))
     return specs
 
@@ -465,5 +575,5 @@ if __name__ == "__main__":
     selfcheck(specs)
     for name, prog, outs, nw, sch in specs:
         sys.stderr.write("%s: %d products, rounds %s (nw %d), %d slots\n" % (
-            name, len(prog.prods), [len(r) for r in sch["rounds"]], nw, sch["nslots"]))
+            name, len(prog.prods), [sum(i is not None for i in r) for r in sch["rounds"]], nw, sch["nslots"]))
     sys.stdout.write("\n".join(emit(specs)) + "\n")

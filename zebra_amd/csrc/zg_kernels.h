@@ -20,7 +20,7 @@ namespace zg {
 //   k_batch_fchain: the f-chain (sparse line product, then squaring, fused per step)
 //                   -> ftree leaves
 // A block = 64 proofs; NW waves share each round's independent Fq2 products.
-#define ZG_LINES_NW 6   // widest round of dbl/add
+#define ZG_LINES_NW 4   // one wave per SIMD, 13 LDS slots: two blocks share a CU
 #define ZG_FC_NW 8      // 2 waves per SIMD (256 VGPRs, no spills); msq = 4 rounds
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
 #define ZG_PUB_STEPS 4  // fused launch: lines steps per publish
@@ -30,7 +30,9 @@ __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
 }
 
 // lines layout: [step][proof][A, B, C]
-// LDS slots (both programs): 0 X, 1 Y, 2 Z, 3 PQ = (px, py) (kept), add: 4 QX, 5 QY
+// LDS slots (both programs): 0 X, 1 Y, 2 Z, 3 PQ = (px, py) (kept); add reads QX, QY (B) from
+// HBM (AtomSpace::q). Line coefficients B, C are stored to HBM by the waves of their products
+// (ZG_LINES_SINK_MASK), A after the output round.
 // The R-chain of pairing's G2Prepared is the double-and-add of [x] B (x = |u|, Jacobian), so
 // the G2 subgroup check of B (psi(B) = [u] B, zg_curve.h) is its last step here: a B that
 // fails it turns its proof DECODE_INVALID (Proof::read) and its leaves back to the identity.
@@ -41,6 +43,8 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
   const int proof = blk * 64 + lane;
   const bool act = proof_active(b, proof);
   const bool chk = proof < b.n && !b.ptB[proof].inf;  // B owes its subgroup check
+  static_assert(ZG_LINES_SINK_MASK == 0x30, "lines outputs 4, 5 (B, C) are stored by their products");
+  const AtomSpace atq{at.base, &b.ptB[chk ? proof : 0].x};  // add: QX, QY from HBM
   if (wave == 0) {
     G2A q;
     G1A p;
@@ -65,21 +69,15 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
     for (int pass = 0; pass < 2; pass++) {
       if (pass == 1 && (i < 0 || !((ZG_XH >> i) & 1ull))) break;
       const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
-      if (pid == ZG_PROG_ADD) {
-        if (wave < 2) {
-          const G2A q = b.ptB[chk ? proof : 0];
-          at.put(4 + wave, wave == 0 ? (chk ? q.x : f2_one()) : (chk ? q.y : f2_one()));
-        }
-        __syncthreads();
-      }
-      prog_run(pid, at);
+      Fq2* sink = proof < b.npad ? lines + ((size_t)n * b.npad + proof) * 3 : nullptr;
+      prog_run<true>(pid, atq, sink, act);
       Fq2 v;
-      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      if (wave < 4) v = prog_output(PROG_INFO[pid].go + wave, atq);
       __syncthreads();
       if (wave < 3)
         at.put(wave, v);
-      else if (wave < 6 && proof < b.npad)
-        lines[((size_t)n * b.npad + proof) * 3 + (wave - 3)] = act ? v : f2_one();
+      else if (wave == 3 && sink)
+        sink[0] = act ? v : f2_one();
       // publish every ZG_PUB_STEPS steps: each wave's stores released, then the count
       const bool pub = prog && ((n + 1) % ZG_PUB_STEPS == 0 || n + 1 == ZG_NCOEFF);
       if (pub) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -105,7 +103,7 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
     }
   }
 }
-__global__ void __launch_bounds__(64 * ZG_LINES_NW) k_batch_lines(BatchBufs b, Fq2* lines) {
+__global__ void __launch_bounds__(64 * ZG_LINES_NW, 2) k_batch_lines(BatchBufs b, Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
   lines_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr);
 }
@@ -174,7 +172,7 @@ __device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_MM : ZG_PROG_MMSQ);
-      prog_run(pid, at);
+      prog_run<false>(pid, at);
       Fq2 v;
       if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
       __syncthreads();
@@ -248,7 +246,7 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, cons
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
-      prog_run(pid, at);
+      prog_run<false>(pid, at);
       Fq2 v;
       if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
       __syncthreads();
