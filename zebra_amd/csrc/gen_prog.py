@@ -550,7 +550,7 @@ def build_all():
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         if fn in (prog_mmsq, prog_mm):
-            sch = schedule(prog, outs, nw, 3000, 25)
+            sch = schedule(prog, outs, nw, 3000, 25, cost=True)
         elif fn in (prog_dbl, prog_add):
             sch = schedule(prog, outs, nw, 6000, LINES_MAX_SLOTS, shift=0, partial=True)
             assert sch["nslots"] <= LINES_MAX_SLOTS, (prog.name, sch["nslots"])
