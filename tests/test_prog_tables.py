@@ -95,3 +95,13 @@ def test_coop_tables():
     c = B.f12_mul(B.f12_conj(a), B.f12_inv(a))
     c = B.f12_mul(B.f12_frob(c, 2), c)
     assert gen_coop.evaluate(ops["csqr"], B.f12_coeffs(c), None) == B.f12_coeffs(B.f12_sqr(c))
+
+
+def test_lazy_operand_forms():
+    """the emitted lazy operand forms (plain 12-word sums with K p offsets, never reduced) and
+    the products' ZG_KIND codes, interpreted on extreme (0, p - 1) and random atoms: every carry
+    chain stays within [0, 2^384), operands equal the forms mod p, outputs are canonical, and the
+    raw product bounds fit the conditional subtractions / quotient estimate the code selects"""
+    if not gen_prog.LAZY:
+        return
+    gen_prog.check_lazy(gen_prog.build_all(), trials=12)

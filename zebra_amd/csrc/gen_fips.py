@@ -109,7 +109,17 @@ def op_lzsub(tag, r, a, b):
     return ins, ["%sd%d" % (tag, i) for i in range(N)], [tag + "k0", tag + "k1"]
 
 
-OPS = {"add": op_add, "sub": op_sub, "lzadd": op_lzadd, "lzsub": op_lzsub}
+def op_psub(tag, r, a, b):
+    """r = a - b (no reduction; the caller guarantees a >= b)"""
+    ins = []
+    for i in range(N):
+        x = "v_sub_co_u32 %s, %%[%sk0], %s, %s" % (r(i), tag, a(i), b(i)) if i == 0 else \
+            "v_subb_co_u32 %s, %%[%sk0], %s, %s, %%[%sk0]" % (r(i), tag, a(i), b(i), tag)
+        ins.append((x, None if i == 0 else tag + "k0", tag + "k0", tag + "A", i, []))
+    return ins, [], [tag + "k0"]
+
+
+OPS = {"add": op_add, "sub": op_sub, "lzadd": op_lzadd, "lzsub": op_lzsub, "psub": op_psub}
 
 
 def schedule_chains(ops):
@@ -180,7 +190,9 @@ def fq_ops_fn(name, kinds):
 
 FQ_FNS = [("fqa_add", ["add"]), ("fqa_sub", ["sub"]), ("fqa_lzadd", ["lzadd"]), ("fqa_lzsub", ["lzsub"]),
           ("f2a_add", ["add", "add"]), ("f2a_sub", ["sub", "sub"]), ("f2a_lzadd", ["lzadd", "lzadd"]),
-          ("f2a_lzsub", ["lzsub", "lzsub"]), ("f2a_sub_add", ["sub", "add"]), ("f2a_lzadd_lzsub", ["lzadd", "lzsub"])]
+          ("f2a_lzsub", ["lzsub", "lzsub"]), ("f2a_sub_add", ["sub", "add"]), ("f2a_lzadd_lzsub", ["lzadd", "lzsub"]),
+          # plain (unreduced) accumulation steps of the staged engine's lazy operand forms
+          ("f2p_as", ["lzadd", "psub"]), ("f2p_sa", ["psub", "lzadd"]), ("f2p_ss", ["psub", "psub"]), ("fqp_sub", ["psub"])]
 
 
 def gen_mul(name, n, pname, inv, rinv, bound, tbound):

@@ -30,6 +30,22 @@ assert sum(b << (W * i) for i, b in enumerate(P2B)) == 2 * P and all(b >= MASK f
 assert P2B[D - 1] >= (P >> (W * (D - 1)))
 
 
+KP_MAX = 12
+
+
+def borrowed(k):
+    """k p as 14 digits with digits 0..12 raised by 2^29 (borrowed from the next digit)"""
+    q = [((k * P) >> (W * i)) & MASK for i in range(D)]
+    if k == 0:
+        return q
+    b = [q[i] + ((1 << W) if i < D - 1 else 0) - (1 if i > 0 else 0) for i in range(D)]
+    assert sum(x << (W * i) for i, x in enumerate(b)) == k * P and all(x >= MASK for x in b[:D - 1])
+    # dominance: any y < (k - 1) p has top digit <= ((k - 1) p - 1) >> 377 <= b[13]
+    if k >= 2:
+        assert ((k - 1) * P) >> (W * (D - 1)) <= b[D - 1], k
+    return b
+
+
 def split(dst, src):
     out = []
     for L in range(D):
@@ -180,6 +196,36 @@ def main():
     o += fn("f2_sqr29", "uint32_t* c0, uint32_t* c1, const uint32_t* x0, const uint32_t* x1, const uint32_t* dif",
             body, ["x^2 for canonical x given dif = x0 - x1 mod p: c0 = (x0 + x1) dif, c1 = x0 (2 x1). The sum and",
                    "the doubled digits are formed digit-wise (< 2^30). Column bound: 14 terms < 2^59 + 14 m*p."])
+    # ---- raw-output forms for the staged engine's lazy operands (zg_prog.h f2_mul_kind): the
+    # caller bounds the column sum S < M p^2 and finishes the 12-word result t < S / 2^384 + p
+    # (fq_finish: conditional subtractions or a quotient estimate)
+    o.append("#define ZG_KP_MAX %d" % KP_MAX)
+    o.append("// k p (12 words) and k p with borrowed 29-bit digits (digits 0..12 >= 2^29 - 1, top digit")
+    o.append("// >= the top digit of any y <= (k - 1) p), k = 0..%d" % KP_MAX)
+    o.append("static constexpr uint32_t FQ_KP[%d][12] = {%s};" % (KP_MAX + 1, ", ".join(
+        "{%s}" % ", ".join("0x%08xu" % ((k * P >> (32 * i)) & 0xffffffff) for i in range(12)) for k in range(KP_MAX + 1))))
+    o.append("static constexpr uint32_t FQ_KP_B29[%d][14] = {%s};" % (KP_MAX + 1, ", ".join(
+        "{%s}" % ", ".join("0x%08xu" % x for x in borrowed(k)) for k in range(KP_MAX + 1))))
+    o.append("")
+    body = ["  uint32_t X0[14], X1[14], Y0[14], Y1[14], N1[14];"] + split("X0", "x0") + split("X1", "x1") + \
+        split("Y0", "y0") + split("Y1", "y1") + ["  N1[%d] = off[%d] - Y1[%d];" % (i, i, i) for i in range(D)]
+    body += redc([("c0", "a0", lambda k: terms("X0", "Y0", k) + terms("X1", "N1", k)),
+                  ("c1", "a1", lambda k: terms("X0", "Y1", k) + terms("X1", "Y0", k))], canon=False)
+    o += fn("f2_mul29_raw", "uint32_t* c0, uint32_t* c1, const uint32_t* x0, const uint32_t* x1, const uint32_t* y0, "
+            "const uint32_t* y1, const uint32_t* off", body,
+            ["f2_mul29 with y1 <= (k - 1) p and off = FQ_KP_B29[k]: c0 = REDC(x0 y0 + x1 (k p - y1)),",
+             "c1 = REDC(x0 y1 + x1 y0), unreduced (< S / 2^384 + p). x, y < 2^384 (digits < 2^29)."])
+    body = ["  uint32_t X0[14], X1[14], S[14];"] + split("X0", "x0") + split("X1", "x1") + split("S", "s")
+    body += redc([("c0", "a0", lambda k: terms("X0", "S", k)), ("c1", "a1", lambda k: terms("X1", "S", k))],
+                 canon=False)
+    o += fn("f2_mul_fq29_raw", "uint32_t* c0, uint32_t* c1, const uint32_t* x0, const uint32_t* x1, const uint32_t* s",
+            body, ["(x0 s, x1 s), unreduced"])
+    body = ["  uint32_t X0[14], X1[14], D[14], S[14], T[14];"] + split("X0", "x0") + split("X1", "x1") + \
+        split("D", "dif") + ["  S[%d] = X0[%d] + X1[%d];\n  T[%d] = X1[%d] << 1;" % (i, i, i, i, i) for i in range(D)]
+    body += redc([("c0", "a0", lambda k: terms("S", "D", k)), ("c1", "a1", lambda k: terms("X0", "T", k))],
+                 canon=False)
+    o += fn("f2_sqr29_raw", "uint32_t* c0, uint32_t* c1, const uint32_t* x0, const uint32_t* x1, const uint32_t* dif",
+            body, ["x^2 with dif = x0 - x1 + k p (any x < 2^384): c0 = (x0 + x1) dif, c1 = x0 (2 x1), unreduced"])
     o.append("}  // namespace zg")
     sys.stdout.write("\n".join(o) + "\n")
 

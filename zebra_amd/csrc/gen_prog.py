@@ -254,8 +254,29 @@ def _form_instr(f, lazy):
     return n + 74 * (len(terms) - 1)
 
 
+def _lazy_cost(lines, code):
+    n = 0
+    for ln in lines:
+        if ln.startswith(("f2a_lzadd", "f2p_")):
+            n += 24
+        elif "f2_kp" in ln:
+            n += 24
+        elif "f2_reduce_q" in ln:
+            n += 110
+    red = int(code.split(",")[2].strip(" )"))
+    return n + {1: 0, 2: 50, 0: 60}[red]
+
+
 def prod_costs(prog):
     out = []
+    if LAZY:
+        slot = {}  # costs do not depend on the slot map
+        for k in {k for L, R, _ in prog.prods for k in list(L) + list(R)}:
+            slot[k] = ("g", 0) if k[0] == "in" and k[1] in prog.glob else 0
+        for L, R, kind in prog.prods:
+            lines, code = lazy_product(L, R, kind, slot)
+            out.append(PROD_CLK[kind] + 4.4 * _lazy_cost(lines, code))
+        return out
     for L, R, kind in prog.prods:
         c = _form_instr(L, True) + (0 if kind == K_SQR else _form_instr(R, False))
         out.append(PROD_CLK[kind] + 4.4 * c)
@@ -465,6 +486,228 @@ def form_code(f, slot, lazy):
     return acc
 
 
+# ---------------------------------------------------------------- lazy operand forms
+# An operand coefficient is evaluated as a plain 12-word integer: the K p offset that covers its
+# negative terms, plus / minus atom coefficients one unit at a time (f2a_lzadd / f2p_* dual carry
+# chains over both coefficients), never reduced. Its bound B (value <= B p) is the number of units
+# (<= 9 so that it stays below 2^384); a longer form is reduced mid-way (fq_reduce_q). The product
+# gets ZG_KIND(kind, k, red) from the bounds: red conditional subtractions (or 0: fq_reduce_q)
+# bring its raw result t < S / 2^384 + p, S <= M p^2, back below p.
+LAZY = True
+SEG_FIRST, SEG_NEXT = 9, 8
+KMAX = 12
+
+
+def lazy_form(f, slot, var, canon):
+    """C++ lines assigning Fq2 `var` from form f; returns (lines, bound B). Atoms are read from
+    LDS right before their first unit (short live ranges)."""
+    items = sorted(f.items(), key=lambda kv: (1, slot[kv[0]][1]) if isinstance(slot[kv[0]], tuple) else (0, slot[kv[0]]))
+    ref = lambda k: "at.q(%d)" % slot[k][1] if isinstance(slot[k], tuple) else "at.get(%d)" % slot[k]
+    if len(items) == 1 and items[0][1] == (1, 0):
+        return ["%s = %s;" % (var, ref(items[0][0]))], 1
+    pairs = []  # (atom index, (sign, comp-0 part), (sign, comp-1 part))
+    sg = lambda v: 1 if v > 0 else -1
+    for j, (k, (c0, c1)) in enumerate(items):
+        pairs += [(j, (sg(c0), ".c0"), (sg(c0), ".c1"))] * abs(c0)
+        pairs += [(j, (-sg(c1), ".c1"), (sg(c1), ".c0"))] * abs(c1)
+    lines, loaded = [], set()
+    u = lambda j: "%s_u%d" % (var, j)
+
+    def load(j):
+        if j not in loaded:
+            loaded.add(j)
+            lines.append("const Fq2 %s = %s;" % (u(j), ref(items[j][0])))
+    pos, B, first = 0, 0, True
+    while pos < len(pairs):
+        seg = pairs[pos:pos + (SEG_FIRST if first else SEG_NEXT)]
+        pos += len(seg)
+        k0 = sum(1 for p in seg if p[1][0] < 0)
+        k1 = sum(1 for p in seg if p[2][0] < 0)
+        ops = list(seg)
+        if first:
+            if k0 == 0 and k1 == 0:
+                j, a, b = ops.pop(0)
+                load(j)
+                lines.append("%s.c0 = %s%s; %s.c1 = %s%s;" % (var, u(j), a[1], var, u(j), b[1]))
+            else:
+                lines.append("%s = f2_kp<%d, %d>();" % (var, k0, k1))
+            B = len(seg)
+        else:
+            lines.append("%s = f2_reduce_q(%s);" % (var, var))
+            if k0 or k1:
+                lines.append("{ const Fq2 o = f2_kp<%d, %d>(); f2a_lzadd(%s.c0.l, %s.c0.l, o.c0.l, %s.c1.l, %s.c1.l, o.c1.l); }"
+                             % (k0, k1, var, var, var, var))
+            B = 1 + len(seg)
+        for (j, a, b) in ops:
+            load(j)
+            fn = {(1, 1): "f2a_lzadd", (1, -1): "f2p_as", (-1, 1): "f2p_sa", (-1, -1): "f2p_ss"}[(a[0], b[0])]
+            lines.append("%s(%s.c0.l, %s.c0.l, %s%s.l, %s.c1.l, %s.c1.l, %s%s.l);" % (
+                fn, var, var, u(j), a[1], var, var, u(j), b[1]))
+        first = False
+    assert B <= 9
+    if canon:
+        lines.append("%s = f2_reduce_q(%s);" % (var, var) if B >= 2 else
+                     "fq29_canon(%s.c0.l, %s.c0.l); fq29_canon(%s.c1.l, %s.c1.l);" % (var, var, var, var))
+        B = 1
+    return lines, B
+
+
+def fits(M):
+    """the raw product t < M p^2 / 2^384 + p stays below 2^384 (12 words, fq_reduce_q)"""
+    return M * P * P + P * 2 ** 384 < 2 ** 768
+
+
+def red_of(M):
+    """conditional subtractions that bring t < M p^2 / 2^384 + p below p (0: quotient estimate)"""
+    r = -(-M * P // 2 ** 384)
+    return r if r <= 2 else 0
+
+
+def lazy_product(L, R, kind, slot):
+    """(lines, encoded kind expression) for one product"""
+    if kind == K_SQR:
+        lx, bx = lazy_form(L, slot, "x", False)
+        M = 4 * bx * bx
+        if bx > 4 or not fits(M):  # x0 + k p - x1 <= 2 B p must stay below 2^384
+            lx.append("x = f2_reduce_q(x);")
+            bx, M = 1, 4
+        assert fits(M) and 2 * bx * P < 2 ** 384
+        return lx, "ZG_KIND(1, %d, %d)" % (bx, red_of(M))
+    if kind in (K_MULC0, K_MULC1):
+        assert len(R) == 1 and list(R.values())[0] == (1, 0), "the Fq factor is an input atom"
+        lx, bx = lazy_form(L, slot, "x", False)
+        ly, _ = lazy_form(R, slot, "y", False)
+        assert fits(bx)
+        return lx + ly, "ZG_KIND(%d, 0, %d)" % (kind, red_of(bx))
+    best = None
+    for A, Bf in ((L, R), (R, L)):
+        lx, bx = lazy_form(A, slot, "x", False)
+        ly, by = lazy_form(Bf, slot, "y", False)
+        M = bx * (2 * by + 1)
+        cost = (len(lx) + len(ly), M)
+        cand = (not fits(M), red_of(M) == 0, cost, lx, bx, ly, by)
+        if best is None or cand[:3] < best[:3]:
+            best = cand
+    _, _, _, lx, bx, ly, by = best
+    M = bx * (2 * by + 1)
+    while not fits(M):  # too large for 12 words: reduce the larger operand
+        if bx >= by:
+            lx.append("x = f2_reduce_q(x);")
+            bx = 1
+        else:
+            ly.append("y = f2_reduce_q(y);")
+            by = 1
+        M = bx * (2 * by + 1)
+    assert by + 1 <= KMAX and fits(M) and bx <= 9 and by <= 9
+    return lx + ly, "ZG_KIND(0, %d, %d)" % (by + 1, red_of(M))
+
+
+def _run_lines(lines, atoms, env):
+    """interpret the emitted lazy-form lines on integers (exact, with the carry-chain
+    preconditions of every step asserted); atoms: slot -> (c0, c1), global q(j) -> ('g', j)"""
+    import re
+    for ln in lines:
+        for st in [x.strip() for x in ln.replace("{ ", "").replace(" }", "").split(";") if x.strip()]:
+            m = re.match(r"const Fq2 (\w+) = at\.(get|q)\((\d+)\)$", st)
+            if m:
+                env[m.group(1)] = atoms[int(m.group(3)) if m.group(2) == "get" else ("g", int(m.group(3)))]
+                continue
+            m = re.match(r"(\w+) = at\.(get|q)\((\d+)\)$", st)
+            if m:
+                env[m.group(1)] = atoms[int(m.group(3)) if m.group(2) == "get" else ("g", int(m.group(3)))]
+                continue
+            m = re.match(r"(const Fq2 )?(\w+) = f2_kp<(\d+), (\d+)>\(\)$", st)
+            if m:
+                env[m.group(2)] = (int(m.group(3)) * P, int(m.group(4)) * P)
+                continue
+            m = re.match(r"(\w+) = f2_reduce_q\((\w+)\)$", st)
+            if m:
+                v = env[m.group(2)]
+                assert all(0 <= c < 2 ** 384 for c in v)
+                env[m.group(1)] = (v[0] % P, v[1] % P)
+                continue
+            m = re.match(r"(\w+)\.c0 = (\w+)\.(c[01]); (\w+)\.c1 = (\w+)\.(c[01])$", st + "")
+            if m:
+                pass
+            m = re.match(r"(\w+)\.c([01]) = (\w+)\.c([01])$", st)
+            if m:
+                v = list(env.get(m.group(1), (0, 0)))
+                v[int(m.group(2))] = env[m.group(3)][int(m.group(4))]
+                env[m.group(1)] = tuple(v)
+                continue
+            m = re.match(r"(f2a_lzadd|f2p_as|f2p_sa|f2p_ss)\((\w+)\.c0\.l, \w+\.c0\.l, (\w+)\.(c[01])\.l, "
+                         r"\w+\.c1\.l, \w+\.c1\.l, (\w+)\.(c[01])\.l\)$", st)
+            if m:
+                fn, v = m.group(1), list(env[m.group(2)])
+                a0 = env[m.group(3)][int(m.group(4)[1])]
+                a1 = env[m.group(5)][int(m.group(6)[1])]
+                sgn = {"f2a_lzadd": (1, 1), "f2p_as": (1, -1), "f2p_sa": (-1, 1), "f2p_ss": (-1, -1)}[fn]
+                for c, (sg_, aa) in enumerate(zip(sgn, (a0, a1))):
+                    v[c] = v[c] + sg_ * aa
+                    assert 0 <= v[c] < 2 ** 384, (st, v[c])
+                env[m.group(2)] = tuple(v)
+                continue
+            m = re.match(r"fq29_canon\((\w+)\.c([01])\.l, \w+\.c[01]\.l\)$", st)
+            if m:
+                v = list(env[m.group(1)])
+                c = int(m.group(2))
+                assert v[c] < 2 * P
+                v[c] = v[c] - P if v[c] >= P else v[c]
+                env[m.group(1)] = tuple(v)
+                continue
+            raise AssertionError("unparsed: " + st)
+    return env
+
+
+def check_lazy(specs, trials=40):
+    """the emitted lazy forms and product codes, interpreted on extreme and random atoms: every
+    carry-chain precondition holds, operands are the forms' values mod p, and each product's raw
+    result bound matches its ZG_KIND red"""
+    import re
+    rng = random.Random(21)
+    for name, prog, outs, nw, sch in specs:
+        slot = sch["slot"]
+        atoms_needed = set(v for v in slot.values() if not (isinstance(v, tuple) and v[0] == "sink"))
+        for t in range(trials):
+            pick = [lambda: 0, lambda: P - 1, lambda: rng.randrange(P)][t % 3] if t < 6 else (lambda: rng.choice([0, P - 1, rng.randrange(P)]))
+            atoms = {a: (pick(), pick()) for a in atoms_needed}
+            val = lambda f: tuple(sum(((c0 * atoms[slot[k]][0] - c1 * atoms[slot[k]][1]) if comp == 0 else
+                                       (c0 * atoms[slot[k]][1] + c1 * atoms[slot[k]][0])) for k, (c0, c1) in f.items()) % P
+                                  for comp in (0, 1))
+            for i, (L, R, kind) in enumerate(prog.prods):
+                lines, code = lazy_product(L, R, kind, slot)
+                env = _run_lines(lines, atoms, {})
+                kd, k, red = map(int, re.match(r"ZG_KIND\((\d+), (\d+), (\d+)\)", code).groups())
+                x = env["x"]
+                assert all(0 <= c < 2 ** 384 for c in x)
+                if kd == 1:
+                    assert (x[0] % P, x[1] % P) == val(L)
+                    d = x[0] + k * P
+                    assert d < 2 ** 384
+                    d -= x[1]
+                    assert d >= 0
+                    S = [(x[0] + x[1]) * d, x[0] * 2 * x[1]]
+                else:
+                    y = env["y"]
+                    assert all(0 <= c < 2 ** 384 for c in y)
+                    assert {(x[0] % P, x[1] % P), (y[0] % P, y[1] % P)} <= {val(L), val(R)} or kd != 0
+                    if kd == 0:
+                        assert y[1] <= (k - 1) * P
+                        S = [x[0] * y[0] + x[1] * (k * P - y[1]), x[0] * y[1] + x[1] * y[0]]
+                    else:
+                        S = [x[0] * y[0], x[1] * y[0]] if kd == 2 else [x[0] * y[1], x[1] * y[1]]
+                for Sc in S:
+                    assert Sc >= 0
+                    tmax = Sc // 2 ** 384 + P  # t < S / 2^384 + p
+                    assert tmax <= (2 ** 384 if red == 0 else (red + 1) * P), (name, i, red)
+            for j, f in enumerate(outs):
+                if j in sch.get("sinks", {}).values():
+                    continue
+                lines, _ = lazy_form(f, slot, "v", True)
+                env = _run_lines(lines, atoms, {})
+                assert env["v"] == val(f) and all(c < P for c in env["v"]), (name, j)
+
+
 def emit(specs):
     out = ["// GENERATED by zebra_amd/csrc/gen_prog.py -- do not edit.", "#pragma once",
            "// included by zg_prog.h (needs AtomSpace and the Fq2 helpers)", "namespace zg {"]
@@ -476,6 +719,14 @@ def emit(specs):
         # products
         for i, (L, R, kind) in enumerate(prog.prods):
             s = sch["slot"]
+            if LAZY:
+                d = s[("p", i)]
+                dst = SINK_BASE + d[1] if isinstance(d, tuple) else d
+                lines, code = lazy_product(L, R, kind, s)
+                prod_cases.append("  case %d: {  // %s p%d round %d%s\n    %s\n    dst = %d; return %s;\n  }" % (
+                    gk + i, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else "",
+                    "\n    ".join(lines), dst, code))
+                continue
             if kind == K_SQR:
                 x, y = form_code(L, s, False), "x"
             elif kind in (K_MULC0, K_MULC1):
@@ -494,6 +745,10 @@ def emit(specs):
         for j, f in enumerate(outs):
             if j in sch.get("sinks", {}).values():
                 out_cases.append("  case %d: return f2_zero();  // %s out %d: stored by its product" % (go + j, name, j))
+            elif LAZY:
+                lines, _ = lazy_form(f, sch["slot"], "v", True)
+                out_cases.append("  case %d: {  // %s out %d\n    Fq2 v;\n    %s\n    return v;\n  }" % (
+                    go + j, name, j, "\n    ".join(lines)))
             else:
                 out_cases.append("  case %d: return %s;  // %s out %d" % (go + j, form_code(f, sch["slot"], False),
                                                                         name, j))
@@ -504,6 +759,7 @@ def emit(specs):
                       sch["rb"]))
         gk += len(prog.prods)
         go += len(outs)
+    out.append("#define ZG_PROG_LAZY %d  // operands as lazy forms, products return ZG_KIND codes" % int(LAZY))
     out.append("struct ProgInfo { int nin, nprod, nout, nrounds, nw, sched, gk, go, nslots, rb; };")
     for k, (name, nin, npr, nout, nr, nw, off, g1, g2, ns, rb) in enumerate(infos):
         out.append("#define ZG_PROG_%s %d  // %d products in %d rounds of %d waves, %d LDS slots%s" % (
@@ -573,6 +829,8 @@ def selfcheck(specs):
 if __name__ == "__main__":
     specs = build_all()
     selfcheck(specs)
+    if LAZY:
+        check_lazy(specs)
     for name, prog, outs, nw, sch in specs:
         sys.stderr.write("%s: %d products, rounds %s (nw %d), %d slots\n" % (
             name, len(prog.prods), [sum(i is not None for i in r) for r in sch["rounds"]], nw, sch["nslots"]))
