@@ -208,9 +208,11 @@ def main():
     # --dist: the RCCL path even at world size 1 (a 1-GPU rehearsal of the multi-GPU protocol)
     use_dist = world > 1 or args.dist
     if args.inflight <= 0:
-        # at most 6 contexts per process (7 fail with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box,
-        # whatever the queue count): deferred verdicts spend one on the checker
-        args.inflight = 3 if args.n // world > 16384 else (6 if args.sync_verdict else 5)
+        # small shards need more batches on the device to fill it (8k-proof shards, round 2:
+        # 4 -> 3.54, 5 -> 3.28, 6 -> 3.20, 8 -> 3.25, 10 -> 3.63 ms per batch; profiles/r02l_inflight_sweep.txt);
+        # the slots share the device's fixed stream pool, so the round-1 limit of
+        # 6 contexts per process no longer applies
+        args.inflight = 3 if args.n // world > 16384 else 6
     # two streams per context (main + side): give each its own hardware queue (set before the
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     # (RCCL's own streams want queues too: 8k shard over RCCL 5.58 ms/batch at 12 queues, 4.70 at 24)
