@@ -42,6 +42,9 @@ def test_prog_schedule_structure():
             assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
             # B and C (outputs 4, 5) leave through their products' waves: no slot
             assert sorted(sch["sinks"].values()) == [4, 5], name
+        elif name in ("q4sq", "q4"):
+            # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse
+            assert sch["nslots"] <= 25 and sch["rb"] == 1, name
         else:
             # no read barrier: a slot is never written in the round that reads its previous content
             assert sch["rb"] == 0, name
@@ -77,6 +80,14 @@ def test_fchain_programs():
         fl = B.f12_mul(f, line)
         assert run("m", f12_pairs(f) + [A, Bc, C]) == f12_pairs(fl)
         assert run("msq", f12_pairs(f) + [A, Bc, C]) == f12_pairs(B.f12_sqr(fl))
+        # four proofs per lane: f * l0 * l1 * l2 * l3 (then squared)
+        ls = [(rnd2(rng), rnd2(rng), rnd2(rng)) for _ in range(4)]
+        f4 = f
+        for (a_, b_, c_) in ls:
+            f4 = B.f12_mul(f4, ((a_, b_, B.F2_ZERO), (B.F2_ZERO, c_, B.F2_ZERO)))
+        flat = [x for l in ls for x in l]
+        assert run("q4", f12_pairs(f) + flat) == f12_pairs(f4)
+        assert run("q4sq", f12_pairs(f) + flat) == f12_pairs(B.f12_sqr(f4))
 
 
 def test_coop_tables():

@@ -228,6 +228,28 @@ def prog_mm():
     return p, m014(p, f1, ins[9], ins[10], ins[11])
 
 
+def prog_q4sq():
+    """four-proof f-chain step: f = (f * l_0 * l_1 * l_2 * l_3)^2, the squaring shared by the
+    four proofs of one lane (64 products instead of 2 x 38 for two pairs).
+    in: F0..F5, then A B C of proofs 4j .. 4j+3."""
+    p = Prog("q4sq", ["F%d" % i for i in range(6)] + ["%s%d" % (c, j) for j in range(4) for c in "ABC"])
+    ins = [p.inp(i) for i in range(18)]
+    f = ins[0:6]
+    for j in range(4):
+        f = m014(p, f, ins[6 + 3 * j], ins[7 + 3 * j], ins[8 + 3 * j])
+    return p, f12_sqr(p, f)
+
+
+def prog_q4():
+    """four-proof f-chain step without the squaring."""
+    p = Prog("q4", ["F%d" % i for i in range(6)] + ["%s%d" % (c, j) for j in range(4) for c in "ABC"])
+    ins = [p.inp(i) for i in range(18)]
+    f = ins[0:6]
+    for j in range(4):
+        f = m014(p, f, ins[6 + 3 * j], ins[7 + 3 * j], ins[8 + 3 * j])
+    return p, f
+
+
 # ---------------------------------------------------------------- scheduling + slots
 # Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
 # Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
@@ -774,7 +796,7 @@ def emit(specs):
     out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
                sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
     out.append("// operands of global product gk; returns the product kind (f2_mul_kind)")
     out.append("__device__ __forceinline__ int prog_operands(int gk, const AtomSpace& at, Fq2& x, Fq2& y, int& dst) {")
@@ -802,11 +824,14 @@ LINES_MAX_SLOTS = 13
 def build_all():
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
-                   (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN)):
+                   (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         if fn in (prog_mmsq, prog_mm):
             sch = schedule(prog, outs, nw, 3000, 25, cost=True)
+        elif fn in (prog_q4sq, prog_q4):  # 18 inputs: only the same-round slot reuse fits 25 slots
+            sch = schedule(prog, outs, nw, 3000, 25, shift=0, partial=True, cost=True)
+            assert sch["nslots"] <= 25, (prog.name, sch["nslots"])
         elif fn in (prog_dbl, prog_add):
             sch = schedule(prog, outs, nw, 6000, LINES_MAX_SLOTS, shift=0, partial=True)
             assert sch["nslots"] <= LINES_MAX_SLOTS, (prog.name, sch["nslots"])

@@ -30,6 +30,7 @@ using namespace zg;
 #define ZG_NTIMINGS 9
 #define ZG_NSTATS 7
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
+#define ZG_QUAD_MIN 32768        // shards from this many (padded) proofs run the f-chain four proofs per lane
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
 
 namespace zg {  // zg_merkle.hip
@@ -138,6 +139,8 @@ struct zg_ctx {
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
+  int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
+  int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
   // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
@@ -252,6 +255,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   ctx->side = dev->side[ctx->pair];
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
+  if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
     if (e == hipSuccess) e = r;
@@ -708,6 +712,10 @@ static int run_pipeline(zg_ctx* ctx) {
                      (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu &&
                       ctx->dev->inflight.load(std::memory_order_relaxed) == 0);
   ctx->fused_last = fused;
+  // four proofs per lane on large shards (one block per CU from 64k proofs on): 64 Fq2 products
+  // per four proofs and step instead of 76 (k_batch_fchain4)
+  const bool quads = !fused && ctx->npad >= 4 && (ctx->quads == 1 || (ctx->quads < 0 && ctx->npad >= ZG_QUAD_MIN));
+  ctx->quads_last = quads;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
@@ -720,12 +728,16 @@ static int run_pipeline(zg_ctx* ctx) {
     hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
-    hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
-                       (const Fq2*)ctx->d_lines, (const int*)nullptr);
+    if (quads)
+      hipLaunchKernelGGL(k_batch_fchain4, dim3((unsigned)((ctx->npad / 4 + 63) / 64)), dim3(64 * ZG_FC_NW), 0,
+                         ctx->stream, b, (const Fq2*)ctx->d_lines);
+    else
+      hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
+                         (const Fq2*)ctx->d_lines, (const int*)nullptr);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  for (size_t lo = ctx->npad / 4; lo >= 1; lo /= 2) {
+  for (size_t lo = ctx->npad / (quads ? 8 : 4); lo >= 1; lo /= 2) {
     if (lo >= ZG_TREE_COOP_BELOW)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
@@ -1018,6 +1030,14 @@ static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st, bool root_failed) {
   while (!fails.empty() && d < depth_leaf) {
     int k = 1;
     while (k < depth_leaf - d && fails.size() * (size_t)(2 << k) <= ZG_BISECT_BUDGET) k++;
+    // four proofs per lane wrote no pair-level nodes: go from the quad level (or above) straight
+    // to the leaves, or stop one level higher
+    if (ctx->quads_last && d + k == depth_leaf - 1) {
+      if (k > 1 && fails.size() * (size_t)(2 << (k + 1)) > ZG_BISECT_BUDGET)
+        k--;
+      else
+        k++;
+    }
     std::vector<int> level;
     for (int node : fails)  // descendants that start at or beyond n hold only padding: skipped
       for (int c = node << k; c < (node + 1) << k; c++)

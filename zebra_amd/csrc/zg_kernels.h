@@ -199,6 +199,58 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, con
   fchain_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr, nullptr);
 }
 
+// Four proofs per lane (large shards, ZG_QUAD_MIN): the quad (4j .. 4j+3) shares one Miller
+// accumulator, f <- (f l_4j l_4j+1 l_4j+2 l_4j+3)^2 per step (staged programs Q4SQ / Q4: 64 Fq2
+// products per quad-step where two pairs need 76), and the kernel writes the tree level of proof
+// quads (npad/4 nodes; bisection never stops at the pair level below it, zg.hip bisect).
+// LDS slots 0..5 f, 6..17 the four line triples; atom j of a step's lines is loaded by wave
+// (j + 6) mod 8, alongside waves 0..5 storing the f outputs.
+__device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* lines, int blk, const AtomSpace& at) {
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int quad = blk * 64 + lane;
+  const bool inb = quad < b.npad / 4;
+  int actm = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) actm |= (inb && proof_active(b, 4 * quad + j)) ? 1 << j : 0;
+  auto load_lines = [&](int n) {
+    const Fq2* src = lines + ((size_t)n * b.npad + 4 * (size_t)quad) * 3;
+    for (int j = (wave + 2) & 7; j < 12; j += 8) {
+      const bool act = (actm >> (j / 3)) & 1;
+      at.put(6 + j, act ? src[j] : (j % 3 == 0 ? f2_one() : f2_zero()));
+    }
+  };
+  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  load_lines(0);
+  __syncthreads();
+  int n = 0;
+  for (int i = ZG_XH_TOP;; i--) {
+    const bool last = i < 0;
+    const bool addbit = !last && ((ZG_XH >> i) & 1ull);
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_Q4 : ZG_PROG_Q4SQ);
+      prog_run<true>(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      __syncthreads();
+      n++;
+      if (wave < 6) at.put(wave, v);
+      if (n < ZG_NCOEFF) load_lines(n);
+      __syncthreads();
+    }
+    if (last) break;
+  }
+  // conjugate (u < 0) and store the quad node
+  if (wave < 6 && inb) {
+    Fq2 v = at.get(wave);
+    if (wave >= 3) v = f2_neg(v);
+    reinterpret_cast<Fq2*>(&b.ftree[b.npad / 4 + quad])[wave] = v;
+  }
+}
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, const Fq2* lines) {
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  fchain4_body(b, lines, blockIdx.x, AtomSpace{lds_atoms});
+}
+
 // The R-chain and the f-chain as ONE launch for shards whose two grids fit on the device at
 // once (an 8,192-proof rank: 128 lines blocks + 64 f-chain blocks, one block per CU by LDS):
 // blocks [0, P) run the lines of 64 proofs and publish each step (release, agent scope);
