@@ -366,7 +366,9 @@ def main():
     if not iso:
         iso = timings
     fused = iso[0][1] < 0.05   # the fused launch leaves the lines phase empty (isolated pass)
-    rk, wk = ("k_lines_fchain", W_LINES + W_FCHAIN) if fused else ("k_batch_fchain", W_FCHAIN)
+    quads = ctx.stats().get("quad_fchain_launches", 0) > 0  # four proofs per lane (k_batch_fchain4)
+    rk, wk = ("k_lines_fchain", W_LINES + W_FCHAIN) if fused else \
+        ("k_batch_fchain4" if quads else "k_batch_fchain", W_FCHAIN)
     achieved = wk * MACS_PER_FQMUL * shard / (avg[2] * 1e-3)
     iso_avg = [sum(t[i] for t in iso) / len(iso) for i in range(NP)]
     iso_achieved = wk * MACS_PER_FQMUL * shard / (iso_avg[2] * 1e-3)

@@ -277,7 +277,9 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * split kernel; the context uses split launches from then on), [3] batches with a B that
  * failed its G2 subgroup check (gated recompute of the VK-side root work), [4] bisections,
  * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
- * non-zero window digit, summed over the windows). Writes min(n, 7) values, zero beyond. */
+ * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
+ * (k_batch_fchain4; shards from 32,768 padded proofs, ZG_FCHAIN_QUADS). Writes min(n, 8) values,
+ * zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

@@ -158,10 +158,14 @@ def test_config3_exact_reject_set(workload3, cpu):
     c = Context(device=0, max_batch=65536)
     try:
         sts, _ = c.verify_batch(bp, kinds, bx)
+        st = c.stats()
     finally:
         c.close()
     got = {i: s for i, s in enumerate(sts) if s != 0}
     assert got == want
+    # the 64k shard ran the four-proofs-per-lane f-chain, and bisection descended through its
+    # quad-level tree (no pair-level nodes) to the exact reject set
+    assert st["quad_fchain_launches"] >= 1 and st["bisections"] == 1
 
 
 def _shards_run(ctxs, proofs, kinds, inputs, shard):

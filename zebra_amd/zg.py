@@ -266,7 +266,7 @@ class Context:
         return list(a)
 
     STAT_NAMES = ("batches", "fused_launches", "fused_wait_failures", "b_subgroup_recomputes", "bisections",
-                  "bisect_nodes", "k4_entries")
+                  "bisect_nodes", "k4_entries", "quad_fchain_launches")
 
     def stats(self):
         """cumulative counters (include/zg.h zg_stats) as a dict"""
