@@ -124,6 +124,37 @@ def redc(chains, canon=True):
     return out
 
 
+def redc_full(chains):
+    """full-radix FIPS reduction by 2^406 (14 digits of 29 bits): results as 14 normalized digits
+    in out_name (digit-resident chains: no split / repack between products)"""
+    out = []
+    for (r, a, _) in chains:
+        out.append("  uint32_t %s_m[14];" % a)
+        out.append("  uint64_t %s = 0;" % a)
+    for k in range(2 * D - 1):
+        cols = [(r, a, f(k)) for (r, a, f) in chains]
+        n = max(len(t) for _, _, t in cols)
+        for q in range(n):
+            for (r, a, t) in cols:
+                if q < len(t):
+                    x, i, y, j = t[q]
+                    out.append("  %s += (uint64_t)%s[%d] * %s[%d];" % (a, x, i, y, j))
+        for j in range(D):
+            if j < k and k - j < D:
+                for (r, a, _) in cols:
+                    out.append("  %s += (uint64_t)%s_m[%d] * 0x%08xu;" % (a, a, j, P29[k - j]))
+        for (r, a, _) in cols:
+            if k < D:
+                out.append("  %s_m[%d] = ((uint32_t)%s * 0x%08xu) & FQ29_MASK;" % (a, k, a, PINV))
+                out.append("  %s += (uint64_t)%s_m[%d] * 0x%08xu;" % (a, a, k, P29[0]))
+            else:
+                out.append("  %s[%d] = (uint32_t)%s & FQ29_MASK;" % (r, k - D, a))
+            out.append("  %s >>= 29;" % a)
+    for (r, a, _) in chains:
+        out.append("  %s[13] = (uint32_t)%s;" % (r, a))
+    return out
+
+
 def fn(name, args, body, doc):
     return ["// " + d for d in doc] + ["ZG_INL void %s(%s) {" % (name, args)] + body + ["}", ""]
 
@@ -196,6 +227,40 @@ def main():
     o += fn("f2_sqr29", "uint32_t* c0, uint32_t* c1, const uint32_t* x0, const uint32_t* x1, const uint32_t* dif",
             body, ["x^2 for canonical x given dif = x0 - x1 mod p: c0 = (x0 + x1) dif, c1 = x0 (2 x1). The sum and",
                    "the doubled digits are formed digit-wise (< 2^30). Column bound: 14 terms < 2^59 + 14 m*p."])
+    # ---- digit-resident products (Montgomery R' = 2^406, 14 normalized digits in and out): chains
+    # of products (exponentiations) skip the split / repack / canonicalisation of every product
+    RP = 2 ** (D * W)
+    kin = (2 ** (2 * D * W - 384)) % P    # a R -> a R' : REDC'(a R * kin)
+    kout = (2 ** 384) % P                  # a R' -> a R : REDC'(a R' * kout)
+    o.append("static constexpr uint32_t FQ29D_KIN[14] = {%s};  // 2^428 mod p: R -> R' = 2^406" %
+             ", ".join("0x%08xu" % ((kin >> (W * i)) & MASK) for i in range(D)))
+    o.append("static constexpr uint32_t FQ29D_KOUT[14] = {%s};  // 2^384 mod p: R' -> R" %
+             ", ".join("0x%08xu" % ((kout >> (W * i)) & MASK) for i in range(D)))
+    o.append("")
+    body = redc_full([("r", "acc", lambda k: terms("a", "b", k))])
+    o += fn("fq29d_mul", "uint32_t* r, const uint32_t* a, const uint32_t* b", body,
+            ["r = a b 2^-406 mod p in digits: a, b < 2p (normalized digits) -> r < 2p (normalized).",
+             "r may alias neither a nor b."])
+    body = ["  uint32_t A2[14];"] + ["  A2[%d] = a[%d] << 1;" % (i, i) for i in range(D)]
+    body += redc_full([("r", "acc", lambda k: sq_terms("a", "A2", k))])
+    o += fn("fq29d_sqr", "uint32_t* r, const uint32_t* a", body,
+            ["r = a^2 2^-406 mod p in digits (a < 2p) -> r < 2p; r may not alias a."])
+    body = ["  uint32_t A[14];"] + split("A", "a")
+    body += redc_full([("r", "acc", lambda k: terms("A", "FQ29D_KIN", k))])
+    o += fn("fq29d_from_mont", "uint32_t* r, const uint32_t* a",
+            body, ["12-word a R (any a < 2^384) -> 14-digit a R' (< 2p)"])
+    body = ["  uint32_t u[14], t[12];"] + redc_full([("u", "acc", lambda k: terms("a", "FQ29D_KOUT", k))])
+    for w in range(12):
+        b_ = 32 * w
+        L, o_ = b_ // W, b_ % W
+        parts = ["(u[%d] >> %d)" % (L, o_) if o_ else "u[%d]" % L, "(u[%d] << %d)" % (L + 1, W - o_)]
+        if o_ + 32 > 2 * W:
+            parts.append("(u[%d] << %d)" % (L + 2, 2 * W - o_))
+        body.append("  t[%d] = %s;" % (w, " | ".join(parts)))
+    body.append("  fq29_canon(r, t);")
+    o += fn("fq29d_to_mont", "uint32_t* r, const uint32_t* a", body,
+            ["14-digit a R' (< 2p) -> canonical 12-word a R"])
+
     # ---- raw-output forms for the staged engine's lazy operands (zg_prog.h f2_mul_kind): the
     # caller bounds the column sum S < M p^2 and finishes the 12-word result t < S / 2^384 + p
     # (fq_finish: conditional subtractions or a quotient estimate)

@@ -428,6 +428,30 @@ ZG_INL Fq fq_inv_fermat(const Fq& a) { return fq_pow_limbs(a, FQ_EXP_INV, 381); 
 // a^((p-3)/4) by the sliding-window chain of zg_constants.h (w = 5: 16 odd powers,
 // 375 squarings + 67 multiplications, vs 379 + 228 for square-and-multiply).
 ZG_NOINL inline void fq_pow_pm3_4_p(Fq* out, const Fq* ap) {
+#if ZG_FQ29
+  // digit-resident chain (Montgomery R' = 2^406, zg_fq29_gen.h fq29d_*): the 375 squarings and 82
+  // multiplications split, repack and canonicalise nothing; one conversion in, one out
+  uint32_t tbl[16][14], a2[14], r[14], t[14];
+  fq29d_from_mont(tbl[0], ap->l);
+  fq29d_sqr(a2, tbl[0]);
+  for (int k = 1; k < 16; k++) fq29d_mul(tbl[k], tbl[k - 1], a2);
+#pragma unroll
+  for (int w = 0; w < 14; w++) r[w] = tbl[FQ_PM3_4_CHAIN[0][1] >> 1][w];
+  for (int i = 1; i < FQ_PM3_4_CHAIN_LEN; i++) {
+    for (int s = 0; s < FQ_PM3_4_CHAIN[i][0]; s++) {
+      fq29d_sqr(t, r);
+#pragma unroll
+      for (int w = 0; w < 14; w++) r[w] = t[w];
+    }
+    const int o = FQ_PM3_4_CHAIN[i][1];
+    if (o) {
+      fq29d_mul(t, r, tbl[o >> 1]);
+#pragma unroll
+      for (int w = 0; w < 14; w++) r[w] = t[w];
+    }
+  }
+  fq29d_to_mont(out->l, r);
+#else
   Fq tbl[16];
   tbl[0] = *ap;
   const Fq a2 = fq_sqr(tbl[0]);
@@ -439,6 +463,7 @@ ZG_NOINL inline void fq_pow_pm3_4_p(Fq* out, const Fq* ap) {
     if (o) r = fq_mul(r, tbl[o >> 1]);
   }
   *out = r;
+#endif
 }
 ZG_INL Fq fq_pow_pm3_4(const Fq& a) {
   Fq r;
