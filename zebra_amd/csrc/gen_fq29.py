@@ -59,6 +59,9 @@ def split(dst, src):
             e = "zg_alignbit(%s[%d], %s[%d], %d) & FQ29_MASK" % (src, w + 1, src, w, o)
         else:
             e = "%s[%d] >> %d" % (src, w, o)
+            out.append("  %s[%d] = %s;" % (dst, L, e))
+            out.append("  zg_opaque(%s[%d]);  // narrow top digit: see gen_mont29" % (dst, L))
+            continue
         out.append("  %s[%d] = %s;" % (dst, L, e))
     return out
 
@@ -100,6 +103,7 @@ def redc(chains, canon=True):
                 out.append("  %s_m[%d] = ((uint32_t)%s * 0x%08xu) & FQ29_MASK;" % (a, k, a, PINV))
             elif k == D - 1:
                 out.append("  %s_m[%d] = ((uint32_t)%s * 0x%08xu) & 127u;" % (a, k, a, PINV))
+                out.append("  zg_opaque(%s_m[%d]);" % (a, k))
         for (r, a, _) in cols:
             if k <= D - 1:
                 out.append("  %s += (uint64_t)%s_m[%d] * 0x%08xu;" % (a, a, k, P29[0]))
@@ -155,6 +159,77 @@ def redc_full(chains):
     return out
 
 
+def gen_mont29(name, M, NW, mname, doc_bound):
+    """generic r = a b 2^(-32 NW) mod M in 29-bit digits (M < 2^(32 NW - 1)): NW words -> D digits,
+    mixed-radix FIPS reduction (D - 1 digits of 29 bits and one of 32 NW - 29 (D - 1)), repack, one
+    conditional subtraction. Column bound: D a*b + D m*M terms < 2^58."""
+    Dm = -(-32 * NW // W)
+    last = 32 * NW - W * (Dm - 1)
+    Md = [(M >> (W * i)) & MASK for i in range(Dm)]
+    pinv = (-pow(M, -1, 1 << W)) % (1 << W)
+    assert 2 * Dm * (1 << 58) < 1 << 64
+    out = ["  uint32_t A[%d], B[%d], m[%d], u[%d], t[%d];" % (Dm, Dm, Dm, Dm + 1, NW), "  uint64_t acc = 0;"]
+    for L in range(Dm):  # split
+        b_ = W * L
+        w, o_ = b_ >> 5, b_ & 31
+        for (X, src) in (("A", "a"), ("B", "b")):
+            if o_ + W <= 32:
+                e = "%s[%d]" % (src, w) if o_ == 0 else "(%s[%d] >> %d)" % (src, w, o_)
+                if o_ + W < 32:
+                    e += " & FQ29_MASK"
+            elif w + 1 < NW:
+                e = "zg_alignbit(%s[%d], %s[%d], %d) & FQ29_MASK" % (src, w + 1, src, w, o_)
+            else:
+                e = "%s[%d] >> %d" % (src, w, o_)
+            out.append("  %s[%d] = %s;" % (X, L, e))
+    # the top digits are narrower than 29 bits; hide their known range from the compiler, whose
+    # gfx950 lowering of 64-bit multiply-adds of two operands known to fit 24 bits gave wrong
+    # results here (found by tools/mb_fr29.hip: the same C is exact on the host)
+    out.append("  zg_opaque(A[%d]); zg_opaque(B[%d]);" % (Dm - 1, Dm - 1))
+    for k in range(2 * Dm - 1):
+        for i in range(Dm):
+            if 0 <= k - i < Dm:
+                out.append("  acc += (uint64_t)A[%d] * B[%d];" % (i, k - i))
+        for j in range(Dm):
+            if j < k and k - j < Dm:
+                out.append("  acc += (uint64_t)m[%d] * 0x%08xu;" % (j, Md[k - j]))
+        if k < Dm - 1:
+            out.append("  m[%d] = ((uint32_t)acc * 0x%08xu) & FQ29_MASK;" % (k, pinv))
+        elif k == Dm - 1:
+            out.append("  m[%d] = ((uint32_t)acc * 0x%08xu) & 0x%08xu;" % (k, pinv, (1 << last) - 1))
+            out.append("  zg_opaque(m[%d]);" % k)
+        if k <= Dm - 1:
+            out.append("  acc += (uint64_t)m[%d] * 0x%08xu;" % (k, Md[0]))
+        if k >= Dm - 1:
+            out.append("  u[%d] = (uint32_t)acc & FQ29_MASK;" % (k - (Dm - 1)))
+        out.append("  acc >>= 29;")
+    out.append("  u[%d] = (uint32_t)acc;  // u = t 2^%d < 2M 2^%d needs a digit more" % (Dm, last, last))
+    for w in range(NW):  # r = u >> last as words
+        b_ = last + 32 * w
+        L, o_ = b_ // W, b_ % W
+        parts = ["(u[%d] >> %d)" % (L, o_) if o_ else "u[%d]" % L]
+        if L + 1 <= Dm:
+            parts.append("(u[%d] << %d)" % (L + 1, W - o_))
+        if o_ + 32 > 2 * W and L + 2 <= Dm:
+            parts.append("(u[%d] << %d)" % (L + 2, 2 * W - o_))
+        out.append("  t[%d] = %s;" % (w, " | ".join(parts)))
+    out += ["#if defined(__HIP_DEVICE_COMPILE__)",
+            "  uint32_t pm[%d];" % NW,
+            "#pragma unroll",
+            "  for (int i = 0; i < %d; i++) pm[i] = %s[i];" % (NW, mname),
+            "  mp_reduce_once<%d>(r, t, pm);" % NW,
+            "#else",
+            "  uint32_t d[%d];" % NW, "  uint64_t bo = 0;",
+            "  for (int i = 0; i < %d; i++) {" % NW,
+            "    const uint64_t x = (uint64_t)t[i] - %s[i] - bo;" % mname,
+            "    d[i] = (uint32_t)x;", "    bo = (x >> 63) & 1;", "  }",
+            "  for (int i = 0; i < %d; i++) r[i] = bo ? t[i] : d[i];" % NW,
+            "#endif"]
+    return fn(name, "uint32_t* r, const uint32_t* a, const uint32_t* b", out,
+              ["r = a b 2^-%d mod %s in 29-bit digits (%d digits, mixed radix: %d x 29 + %d): %s" % (
+                  32 * NW, mname, Dm, Dm - 1, last, doc_bound)])
+
+
 def fn(name, args, body, doc):
     return ["// " + d for d in doc] + ["ZG_INL void %s(%s) {" % (name, args)] + body + ["}", ""]
 
@@ -170,6 +245,14 @@ def main():
           "  return __builtin_amdgcn_alignbit(hi, lo, s);",
           "#else",
           "  return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);",
+          "#endif",
+          "}", ""]
+    o += ["// an optimisation barrier: the compiler forgets what it knows about x's range (no instruction)",
+          "ZG_INL void zg_opaque(uint32_t& x) {",
+          "#if defined(__HIP_DEVICE_COMPILE__)",
+          '  asm volatile("" : "+v"(x));',
+          "#else",
+          "  (void)x;",
           "#endif",
           "}", ""]
     o += ["// r = t >= p ? t - p : t  (t < 2p)",
@@ -260,6 +343,12 @@ def main():
     body.append("  fq29_canon(r, t);")
     o += fn("fq29d_to_mont", "uint32_t* r, const uint32_t* a", body,
             ["14-digit a R' (< 2p) -> canonical 12-word a R"])
+
+    # ---- the 256-bit moduli: BLS12-381 Fr (Jubjub base field) and BN254 Fq (PGHR13)
+    R_BLS = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    P_BN = 0x30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd47
+    o += gen_mont29("fr29_mul", R_BLS, 8, "FR_R", "a, b < r -> r' < r")
+    o += gen_mont29("bq29_mul", P_BN, 8, "BQ_P", "a, b < p -> r < p")
 
     # ---- raw-output forms for the staged engine's lazy operands (zg_prog.h f2_mul_kind): the
     # caller bounds the column sum S < M p^2 and finishes the 12-word result t < S / 2^384 + p

@@ -43,7 +43,9 @@ ZG_NOINL inline u32x8 bq_mul_v(u32x8 a0, u32x8 b0) {
     a.l[i] = a0[i];
     b.l[i] = b0[i];
   }
-#if defined(__HIP_DEVICE_COMPILE__)
+#if ZG_FQ29
+  bq29_mul(r.l, a.l, b.l);  // 29-bit digits (zg_fq29_gen.h; host: same code)
+#elif defined(__HIP_DEVICE_COMPILE__)
   bq_mul_fips(r.l, a.l, b.l);
 #else
   r = fp_mul_inl<BqM>(a, b);

@@ -278,7 +278,9 @@ ZG_NOINL inline u32x8 fr_mul_v(u32x8 a0, u32x8 b0) {
     b.l[i] = b0[i];
   }
   Fr r;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if ZG_FQ29
+  fr29_mul(r.l, a.l, b.l);     // 29-bit digits, carry-free columns (host: same code)
+#elif defined(__HIP_DEVICE_COMPILE__)
   fr_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning
 #else
   r = fp_mul_inl<FrM>(a, b);   // host build of the test harness (tests/native): portable CIOS

@@ -33,11 +33,16 @@ namespace zg {
 #define ZG_PH_TABLE_BYTES ((size_t)ZG_PH_POINTS * ZG_PH_WORDS * 4)
 
 // The Pedersen additions multiply with the inlined product-scanning Montgomery product
-// (fr_mul_fips, ~2 instructions per 32x32 MAC) rather than the out-of-line CIOS fr_mul: a hash
+// (fr29_mul: 29-bit digits, one carry-free v_mad_u64_u32 per digit product; round 1: fr_mul_fips)
+// rather than the out-of-line fr_mul call: a hash
 // group is a lone wave on a latency-bound chain of tree levels, so its time is the number of
 // instructions it issues.
 ZG_INL Fr ph_mul(const Fr& a, const Fr& b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if ZG_FQ29
+  Fr r;
+  fr29_mul(r.l, a.l, b.l);  // 29-bit digits, one carry-free v_mad_u64_u32 per digit product (zg_fq29_gen.h)
+  return r;
+#elif defined(__HIP_DEVICE_COMPILE__)
   Fr r;
   fr_mul_fips(r.l, a.l, b.l);  // gfx950: v_mad_u64_u32 carry-out product scanning (zg_fips.h)
   return r;
