@@ -129,6 +129,24 @@ def test_batch_4096_one_percent_corrupted(ctx):
     assert sts == want
 
 
+def test_batch_4096_corrupted_quad_fchain(ctx, monkeypatch):
+    """the same 41-in-4,096 batch with the four-proofs-per-lane f-chain forced (ZG_FCHAIN_QUADS=1,
+    split launches): the quad tree level has no pair nodes below it, and bisection must still
+    reach the exact reject set; GT of the clean batch equals the pair path's"""
+    from zebra_amd import Context
+    proofs, kinds, inputs, want = corrupted_4096(ctx)
+    monkeypatch.setenv("ZG_FCHAIN_QUADS", "1")
+    monkeypatch.setenv("ZG_LINES_FCHAIN", "0")
+    q = Context(device=0, max_batch=4096)
+    try:
+        sts, _ = q.verify_batch(proofs, kinds, inputs)
+        st = q.stats()
+    finally:
+        q.close()
+    assert sts == want
+    assert st["quad_fchain_launches"] >= 1 and st["fused_launches"] == 0 and st["bisections"] == 1
+
+
 def corrupted_4096(ctx):
     import random
     from zebra_amd import pack_inputs
