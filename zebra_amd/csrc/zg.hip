@@ -28,7 +28,7 @@ using namespace zg;
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 13
 #define ZG_NTIMINGS 9
-#define ZG_NSTATS 7
+#define ZG_NSTATS 8
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_QUAD_MIN 32768        // shards from this many (padded) proofs run the f-chain four proofs per lane
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
@@ -906,6 +906,7 @@ static int collect_batch_stats(zg_ctx* ctx) {
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   ctx->stats[0]++;
   if (ctx->fused_last) ctx->stats[1]++;
+  if (ctx->quads_last) ctx->stats[7]++;
   if (flags[1]) {
     ctx->stats[2]++;
     ctx->fuse_off = 1;
