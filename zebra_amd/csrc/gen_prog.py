@@ -15,6 +15,8 @@ exactly one inlined Fq2-product site). Build tooling; self-checking.
 
     python zebra_amd/csrc/gen_prog.py > zebra_amd/csrc/zg_prog_tables.h
 """
+import json
+import os
 import random
 import sys
 
@@ -353,7 +355,7 @@ def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, c
     return best
 
 
-def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False):
+def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False, fixed=None):
     n = len(prog.prods)
     deps = []
     for L, R, _ in prog.prods:
@@ -378,6 +380,14 @@ def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False):
     rnd = [None] * n
     rounds = []
     done = set()
+    if fixed is not None:  # a cached round assignment (zg_prog_sched.json)
+        for r, pick in enumerate(fixed):
+            for i in pick:
+                assert all(j in done for j in deps[i]), "cached schedule violates a dependency"
+                rnd[i] = r
+            rounds.append(list(pick))
+            done.update(pick)
+        assert len(done) == n
     while len(done) < n:
         ready = [i for i in range(n) if rnd[i] is None and all(j in done for j in deps[i])]
         ready.sort(key=lambda i: (-height[i] + (rng.random() * slack if rng else 0), i))
@@ -821,22 +831,37 @@ NW_FCHAIN = 8
 LINES_MAX_SLOTS = 13
 
 
-def build_all():
+SCHED_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zg_prog_sched.json")
+SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "dbl": 6000, "add": 6000}
+
+
+def build_all(search=None):
+    """search None: the round assignments cached in zg_prog_sched.json where present (checked:
+    dependencies, slot budget); search N: a fresh seeded search of N candidates per program"""
+    cache = {}
+    if search is None and os.path.exists(SCHED_CACHE):
+        cache = json.load(open(SCHED_CACHE))
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
                    (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
-        if fn in (prog_mmsq, prog_mm):
-            sch = schedule(prog, outs, nw, 3000, 25, cost=True)
-        elif fn in (prog_q4sq, prog_q4):  # 18 inputs: only the same-round slot reuse fits 25 slots
-            sch = schedule(prog, outs, nw, 3000, 25, shift=0, partial=True, cost=True)
-            assert sch["nslots"] <= 25, (prog.name, sch["nslots"])
-        elif fn in (prog_dbl, prog_add):
-            sch = schedule(prog, outs, nw, 6000, LINES_MAX_SLOTS, shift=0, partial=True)
-            assert sch["nslots"] <= LINES_MAX_SLOTS, (prog.name, sch["nslots"])
+        shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
+                                       prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
+                                       prog_dbl: (0, True, False, LINES_MAX_SLOTS),
+                                       prog_add: (0, True, False, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
+        if prog.name in cache:
+            sch = _schedule(prog, outs, nw, None, 0, shift, partial,
+                            fixed=[[i for i in r if i is not None] for r in cache[prog.name]])
+            if cost:
+                sch["time"] = balance_rounds(sch, prod_costs(prog), nw)
+        elif slots is not None:
+            n = search if search is not None else SEARCH[prog.name]
+            sch = schedule(prog, outs, nw, n, slots, shift=shift, partial=partial, cost=cost)
         else:
             sch = schedule(prog, outs, nw)
+        if slots is not None:
+            assert sch["nslots"] <= slots, (prog.name, sch["nslots"])
         specs.append((prog.name, prog, outs, nw, sch))
     return specs
 
@@ -852,7 +877,11 @@ def selfcheck(specs):
 
 
 if __name__ == "__main__":
-    specs = build_all()
+    search = int(sys.argv[sys.argv.index("--search") + 1]) if "--search" in sys.argv else None
+    specs = build_all(search)
+    if search is not None:  # record the round assignments (waves in order, None = idle)
+        json.dump({name: sch["rounds"] for name, prog, outs, nw, sch in specs if name in SEARCH},
+                  open(SCHED_CACHE, "w"), indent=0)
     selfcheck(specs)
     if LAZY:
         check_lazy(specs)
