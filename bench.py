@@ -11,7 +11,7 @@ over RCCL (one all-gather), every rank runs the ONE final exponentiation of thei
 same gathered bytes (same verdict, no second collective) and finalises its per-proof statuses. Inputs: real mainnet proofs from the reference's fixtures,
 re-randomized on the GPU (synthetic, all valid; verified OK after the timed region).
 Batch scalars r_i come from the OS RNG inside the timed region (production mode).
-Batches in flight (--inflight; default 3, or 6 on shards <= 16k proofs): each GPU keeps that many
+Batches in flight (--inflight; default 4, or 6 on shards <= 16k proofs): each GPU keeps that many
 consecutive batches on the device, one context (buffers + streams) each. The host reads the
 oldest batch's partial and statuses and relaunches its context at once; the batch's verdict
 (gather + final exponentiation, on a checker context) runs on a worker thread in batch order
@@ -212,7 +212,8 @@ def main():
         # 4 -> 3.54, 5 -> 3.28, 6 -> 3.20, 8 -> 3.25, 10 -> 3.63 ms per batch; profiles/r02l_inflight_sweep.txt);
         # the slots share the device's fixed stream pool, so the round-1 limit of
         # 6 contexts per process no longer applies
-        args.inflight = 3 if args.n // world > 16384 else 6
+        # (65,536-proof shards, r02v: 2 -> 15.95, 3 -> 16.01, 4 -> 15.67, 5 -> 15.83 ms per batch)
+        args.inflight = 4 if args.n // world > 16384 else 6
     # two streams per context (main + side): give each its own hardware queue (set before the
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     # (RCCL's own streams want queues too: 8k shard over RCCL 5.58 ms/batch at 12 queues, 4.70 at 24)
