@@ -307,10 +307,18 @@ def prod_costs(prog):
     return out
 
 
-def balance_rounds(sch, costs, nw):
+def balance_rounds(sch, costs, nw, share=2):
     """order each round's products over the waves so that the two waves of a SIMD (w, w + nw/2)
     carry a heavy and a light product; returns the modelled time (sum over rounds of the
-    busiest SIMD's load)"""
+    busiest SIMD's load). share 1 (the R-chain: one wave per SIMD): a round costs its heaviest
+    product."""
+    if share == 1:
+        total = 0
+        for r, pick in enumerate(sch["rounds"]):
+            srt = sorted([i for i in pick if i is not None], key=lambda i: -costs[i])
+            total += costs[srt[0]] if srt else 0
+            sch["rounds"][r] = srt + [None] * (nw - len(srt))
+        return total
     half = nw // 2
     total = 0
     for r, pick in enumerate(sch["rounds"]):
@@ -325,7 +333,7 @@ def balance_rounds(sch, costs, nw):
     return total
 
 
-def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, cost=False):
+def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, cost=False, share=2):
     """list-schedule products into rounds of <= nw; allocate LDS slots with reuse.
     search > 0: also try that many seeded random tie-breaks among ready products and keep the
     schedule with the fewest rounds whose slots fit max_slots (then the fewest slots).
@@ -335,7 +343,7 @@ def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, c
     best = _schedule(prog, outs, nw, None, 0, shift)
     if cost:
         costs = prod_costs(prog)
-        best["time"] = balance_rounds(best, costs, nw)
+        best["time"] = balance_rounds(best, costs, nw, share)
     if search:
         rng = random.Random(20260101)
         for t in range(search):
@@ -344,7 +352,7 @@ def schedule(prog, outs, nw, search=0, max_slots=None, shift=1, partial=False, c
             fits = max_slots is None or cand["nslots"] <= max_slots
             bfits = max_slots is None or best["nslots"] <= max_slots
             if cost:  # modelled time (SIMD-balanced rounds) instead of the round count
-                cand["time"] = balance_rounds(cand, costs, nw)
+                cand["time"] = balance_rounds(cand, costs, nw, share)
                 key = (not fits, cand["time"], cand["nslots"])
                 bkey = (not bfits, best["time"], best["nslots"])
             else:
@@ -848,16 +856,17 @@ def build_all(search=None):
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
                                        prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
-                                       prog_dbl: (0, True, False, LINES_MAX_SLOTS),
-                                       prog_add: (0, True, False, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
+                                       prog_dbl: (0, True, True, LINES_MAX_SLOTS),
+                                       prog_add: (0, True, True, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
+        share = 1 if fn in (prog_dbl, prog_add) else 2
         if prog.name in cache:
             sch = _schedule(prog, outs, nw, None, 0, shift, partial,
                             fixed=[[i for i in r if i is not None] for r in cache[prog.name]])
             if cost:
-                sch["time"] = balance_rounds(sch, prod_costs(prog), nw)
+                sch["time"] = balance_rounds(sch, prod_costs(prog), nw, share)
         elif slots is not None:
             n = search if search is not None else SEARCH[prog.name]
-            sch = schedule(prog, outs, nw, n, slots, shift=shift, partial=partial, cost=cost)
+            sch = schedule(prog, outs, nw, n, slots, shift=shift, partial=partial, cost=cost, share=share)
         else:
             sch = schedule(prog, outs, nw)
         if slots is not None:
