@@ -540,50 +540,83 @@ KMAX = 12
 
 def lazy_form(f, slot, var, canon):
     """C++ lines assigning Fq2 `var` from form f; returns (lines, bound B). Atoms are read from
-    LDS right before their first unit (short live ranges)."""
+    LDS right before their first use (short live ranges). A coefficient c with |c| >= 2 becomes ONE
+    accumulation of a temporary |c| * atom built by doublings (6 a: 3 dual ops + 1, not 6)."""
     items = sorted(f.items(), key=lambda kv: (1, slot[kv[0]][1]) if isinstance(slot[kv[0]], tuple) else (0, slot[kv[0]]))
     ref = lambda k: "at.q(%d)" % slot[k][1] if isinstance(slot[k], tuple) else "at.get(%d)" % slot[k]
     if len(items) == 1 and items[0][1] == (1, 0):
         return ["%s = %s;" % (var, ref(items[0][0]))], 1
-    pairs = []  # (atom index, (sign, comp-0 part), (sign, comp-1 part))
+    ops = []  # (atom index, weight, (sign, comp-0 part), (sign, comp-1 part))
     sg = lambda v: 1 if v > 0 else -1
-    for j, (k, (c0, c1)) in enumerate(items):
-        pairs += [(j, (sg(c0), ".c0"), (sg(c0), ".c1"))] * abs(c0)
-        pairs += [(j, (-sg(c1), ".c1"), (sg(c1), ".c0"))] * abs(c1)
-    lines, loaded = [], set()
-    u = lambda j: "%s_u%d" % (var, j)
+    for jj, (k, (c0, c1)) in enumerate(items):
+        if c0:
+            ops.append((jj, abs(c0), (sg(c0), ".c0"), (sg(c0), ".c1")))
+        if c1:
+            ops.append((jj, abs(c1), (-sg(c1), ".c1"), (sg(c1), ".c0")))
+    lines, loaded, temps = [], set(), set()
+    u = lambda jj: "%s_u%d" % (var, jj)
 
-    def load(j):
-        if j not in loaded:
-            loaded.add(j)
-            lines.append("const Fq2 %s = %s;" % (u(j), ref(items[j][0])))
-    pos, B, first = 0, 0, True
-    while pos < len(pairs):
-        seg = pairs[pos:pos + (SEG_FIRST if first else SEG_NEXT)]
-        pos += len(seg)
-        k0 = sum(1 for p in seg if p[1][0] < 0)
-        k1 = sum(1 for p in seg if p[2][0] < 0)
-        ops = list(seg)
-        if first:
+    def load(jj):
+        if jj not in loaded:
+            loaded.add(jj)
+            lines.append("const Fq2 %s = %s;" % (u(jj), ref(items[jj][0])))
+
+    def scaled(jj, w):  # the name of w * atom jj (w <= 9: < 9p < 2^384)
+        load(jj)
+        if w == 1:
+            return u(jj)
+        t = "%s_w%d_%d" % (var, jj, w)
+        if t not in temps:
+            temps.add(t)
+            bits = bin(w)[3:]
+            lines.append("Fq2 %s = %s;" % (t, u(jj)))
+            for bit in bits:
+                lines.append("f2a_lzadd(%s.c0.l, %s.c0.l, %s.c0.l, %s.c1.l, %s.c1.l, %s.c1.l);" % ((t,) * 6))
+                if bit == "1":
+                    lines.append("f2a_lzadd(%s.c0.l, %s.c0.l, %s.c0.l, %s.c1.l, %s.c1.l, %s.c1.l);" % (
+                        t, t, u(jj), t, t, u(jj)))
+        return t
+    # segments of at most SEG_FIRST (then SEG_NEXT) units; an op is split across a boundary
+    segs, cur, room, cap = [], [], SEG_FIRST, SEG_FIRST
+    for (jj, w, a, b) in ops:
+        if cur and w > room and w <= SEG_NEXT:  # start a new segment rather than split the op
+            segs.append(cur)
+            cur, room = [], SEG_NEXT
+        while w:
+            take = min(w, room)
+            cur.append((jj, take, a, b))
+            w -= take
+            room -= take
+            if room == 0:
+                segs.append(cur)
+                cur, room = [], SEG_NEXT
+    if cur:
+        segs.append(cur)
+    B = 0
+    for si, seg in enumerate(segs):
+        k0 = sum(w for (jj, w, a, b) in seg if a[0] < 0)
+        k1 = sum(w for (jj, w, a, b) in seg if b[0] < 0)
+        units = sum(w for (jj, w, a, b) in seg)
+        seg = list(seg)
+        if si == 0:
             if k0 == 0 and k1 == 0:
-                j, a, b = ops.pop(0)
-                load(j)
-                lines.append("%s.c0 = %s%s; %s.c1 = %s%s;" % (var, u(j), a[1], var, u(j), b[1]))
+                jj, w, a, b = seg.pop(0)
+                t = scaled(jj, w)
+                lines.append("%s.c0 = %s%s; %s.c1 = %s%s;" % (var, t, a[1], var, t, b[1]))
             else:
                 lines.append("%s = f2_kp<%d, %d>();" % (var, k0, k1))
-            B = len(seg)
+            B = units
         else:
             lines.append("%s = f2_reduce_q(%s);" % (var, var))
             if k0 or k1:
                 lines.append("{ const Fq2 o = f2_kp<%d, %d>(); f2a_lzadd(%s.c0.l, %s.c0.l, o.c0.l, %s.c1.l, %s.c1.l, o.c1.l); }"
                              % (k0, k1, var, var, var, var))
-            B = 1 + len(seg)
-        for (j, a, b) in ops:
-            load(j)
+            B = 1 + units
+        for (jj, w, a, b) in seg:
+            t = scaled(jj, w)
             fn = {(1, 1): "f2a_lzadd", (1, -1): "f2p_as", (-1, 1): "f2p_sa", (-1, -1): "f2p_ss"}[(a[0], b[0])]
             lines.append("%s(%s.c0.l, %s.c0.l, %s%s.l, %s.c1.l, %s.c1.l, %s%s.l);" % (
-                fn, var, var, u(j), a[1], var, var, u(j), b[1]))
-        first = False
+                fn, var, var, t, a[1], var, var, t, b[1]))
     assert B <= 9
     if canon:
         lines.append("%s = f2_reduce_q(%s);" % (var, var) if B >= 2 else
@@ -655,6 +688,10 @@ def _run_lines(lines, atoms, env):
             m = re.match(r"(\w+) = at\.(get|q)\((\d+)\)$", st)
             if m:
                 env[m.group(1)] = atoms[int(m.group(3)) if m.group(2) == "get" else ("g", int(m.group(3)))]
+                continue
+            m = re.match(r"Fq2 (\w+) = (\w+)$", st)
+            if m:
+                env[m.group(1)] = env[m.group(2)]
                 continue
             m = re.match(r"(const Fq2 )?(\w+) = f2_kp<(\d+), (\d+)>\(\)$", st)
             if m:
