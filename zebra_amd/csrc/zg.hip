@@ -141,6 +141,7 @@ struct zg_ctx {
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
+  size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
   // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
@@ -256,6 +257,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
+  if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
     if (e == hipSuccess) e = r;
@@ -738,7 +740,7 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   for (size_t lo = ctx->npad / (quads ? 8 : 4); lo >= 1; lo /= 2) {
-    if (lo >= ZG_TREE_COOP_BELOW)
+    if (lo >= ctx->coop_below)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
       hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
