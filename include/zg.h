@@ -66,6 +66,8 @@ extern "C" {
 #define ZG_E_NOMEM (-5)   /* batch larger than max_batch / allocation failure */
 #define ZG_E_STATE (-6)   /* batch API called out of order */
 #define ZG_E_TREE_FULL (-7) /* TreeState::append: "Appending to full tree" (tree_state.rs:238) */
+#define ZG_E_DEBUG (-8)   /* ZG_DEBUG_EACH=1 (environment, read by zg_create): a batch's statuses differ
+                             from the per-proof verify_proof re-check of the same inputs */
 
 #define ZG_PROOF_BYTES 192
 #define ZG_FR_BYTES 32
@@ -154,7 +156,10 @@ int zg_set_priority(zg_ctx* ctx, int high);
  *                         with the caller, between the rk check and the proof)
  *   zg_prep_output     <- accept_output     verification/src/sapling.rs:171-200 (5 x 32 B out:
  *                         cv.x cv.y epk.x epk.y cmu)
- *   zg_prep_joinsplit  <- sprout::verify    verification/src/sprout.rs:34-58,86-153 (9 x 32 B)
+ *   zg_prep_joinsplit  <- sprout::verify    verification/src/sprout.rs:34-58,86-153 (9 x 32 B,
+ *                         Input::into_bls_frs: the Groth16 branch, 254-bit chunks)
+ *   zg_prep_joinsplit_bn <- the same Input, into_bn_frs (sprout.rs:119-133: 253-bit chunks, 9 x
+ *                         32-byte LE BN254 Fr): the inputs of zg_pghr13_verify for a PHGR JoinSplit
  *   zg_hsig            <- compute_hsig      verification/src/sprout.rs:16-32 */
 #define ZG_PREP_OK 0
 #define ZG_PREP_VALUE_COMMITMENT_INVALID 1     /* ValueCommitment(Invalid) */
@@ -171,6 +176,9 @@ int zg_prep_output(const uint8_t cv[32], const uint8_t cmu[32], const uint8_t ep
 int zg_prep_joinsplit(const uint8_t anchor[32], const uint8_t random_seed[32], const uint8_t nullifiers[64],
                       const uint8_t macs[64], const uint8_t commitments[64], uint64_t vpub_old, uint64_t vpub_new,
                       const uint8_t pubkey[32], uint8_t inputs[9 * 32]);
+int zg_prep_joinsplit_bn(const uint8_t anchor[32], const uint8_t random_seed[32], const uint8_t nullifiers[64],
+                         const uint8_t macs[64], const uint8_t commitments[64], uint64_t vpub_old, uint64_t vpub_new,
+                         const uint8_t pubkey[32], uint8_t inputs[9 * 32]);
 int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32], const uint8_t pubkey[32],
             uint8_t out[32]);
 
@@ -234,8 +242,10 @@ int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uint8_t* state
 /* ---- PGHR13 Sprout proofs on BN254: pre-Sapling JoinSplits (the `bn` crate).
  *   zg_pghr13_vk_load_builtin / _json <- crypto/src/json/pghr13.rs decode of
  *        res/sprout-verifying-key.json (embedded unchanged); points through AffineG1/G2::new
- *        (ZG_E_VK when one is off its curve or, in G2, not of order r). zg_pghr13_verify loads
- *        the builtin key on first use.
+ *        (ZG_E_VK when one is off its curve or, in G2, not of order r). The key is the calling
+ *        context's own: prepared once per distinct key per device into fresh buffers and
+ *        published complete (other contexts keep their keys; a failed load leaves the
+ *        context's key unchanged). zg_pghr13_verify loads the builtin key on first use.
  *   zg_pghr13_verify <- Proof::from_raw + pghr13::verify (crypto/src/pghr13.rs:69-105), called at
  *        verification/src/sprout.rs:61-67: proofs n x 296 bytes (the JoinSplit's PHGR proof),
  *        inputs n x 9 x 32 bytes (BN254 Fr, little-endian: Input::into_bn_frs, 253-bit chunks),
@@ -278,7 +288,8 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * failed its G2 subgroup check (gated recompute of the VK-side root work), [4] bisections,
  * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
  * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
- * (k_batch_fchain4; shards from 32,768 padded proofs, ZG_FCHAIN_QUADS). Writes min(n, 8) values,
+ * (k_batch_fchain4; shards of 8,192 or more padded proofs -- ZG_QUAD_MIN -- or as ZG_FCHAIN_QUADS
+ * forces). Writes min(n, 8) values,
  * zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
@@ -292,6 +303,12 @@ int zg_bench_mad_rate(zg_ctx* ctx, double* macs_per_s);
 /* the same probe, plus the shader clock it ran at (median over workgroups of s_memtime ticks
  * per 100 MHz s_memrealtime tick, stamped around the loop); clock_hz may be NULL */
 int zg_bench_mad_rate_clock(zg_ctx* ctx, double* macs_per_s, double* clock_hz);
+/* debug: the 29-bit-digit Montgomery products every kernel uses, one per lane on `device`, for
+ * exact host comparison (tests/test_gpu_field.py; guards the zg_opaque workaround of DESIGN.md
+ * section 4). field 0: Fq a b 2^-384 mod p (48-B LE operands), 1: Fq a^2 2^-384 (b unused, a < 2p),
+ * 2: Fq2 (96 B = c0 || c1; a lazy < 2p per coefficient, b canonical), 3: BLS12-381 Fr a b 2^-256 mod r
+ * (32 B), 4: BN254 Fq a b 2^-256 mod q (32 B). out has the operands' size. */
+int zg_debug_field_mul(int device, int field, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* out);
 
 #ifdef __cplusplus
 }

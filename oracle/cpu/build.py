@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Build oracle/_build/libzgcpu.so (the CPU restatement of bellman's per-proof path) and
-oracle/_build/libzgmerkle.so (the reference's note-commitment tree path, merkle_cpu.cpp) with
+oracle/_build/libzgmerkle.so (the reference's note-commitment tree path, merkle_cpu.cpp) and
+oracle/_build/libpghr13cpu.so (the reference's PGHR13 check on BN254, pghr13_cpu.cpp) with
 g++ -O3. Test/bench infrastructure only."""
 import os
 import subprocess
@@ -24,9 +25,18 @@ def _gxx(src, lib):
     return lib
 
 
+PGHR13_SRC = os.path.join(HERE, "pghr13_cpu.cpp")
+PGHR13_LIB = os.path.join(OUT, "libpghr13cpu.so")
+
+
 def build():
     _gxx(MERKLE_SRC, MERKLE_LIB)
+    _gxx(PGHR13_SRC, PGHR13_LIB)
     return _gxx(SRC, LIB)
+
+
+def build_pghr13():
+    return _gxx(PGHR13_SRC, PGHR13_LIB)
 
 
 def build_merkle():

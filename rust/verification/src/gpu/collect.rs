@@ -11,12 +11,22 @@
 //!       per spend (prep, spend_auth_sig, proof), per output (prep, proof), binding sig
 //!       -> InvalidSapling; then nullifiers
 //!
-//! The checks that are not Groth16 are evaluated by the caller as today and handed in as
-//! outcomes; every Groth16 proof of the block goes through ONE GpuVerifier::verify call.
-use super::{prep_joinsplit, prep_output, prep_spend, GpuError, GpuVerifier, Item};
+//! The checks that are not proofs or Sapling signatures are evaluated by the caller as today and
+//! handed in as outcomes; every Groth16 proof of the window goes through ONE `Backend::verify`
+//! call and every PHGR JoinSplit proof (sprout.rs:61-67) through ONE `Backend::pghr13_verify`
+//! call. A PHGR failure (InvalidEncoding / InvalidPGHRProof) is InvalidJoinSplit(index) at its
+//! place among the descriptions, before that description's tree_cache.continue_root
+//! (accept_transaction.rs:575-592).
+//!
+//! Backends: `GpuVerifier` (the product) and `cpu::CpuBackend` (the reference's own per-proof
+//! calls). `verify_block_or_cpu` runs the window on the GPU and, on a GpuError, re-runs the
+//! whole window on the CPU backend, so an import never stops on a device fault.
+use super::cpu::CpuBackend;
+use super::{prep_joinsplit, prep_joinsplit_bn, prep_output, prep_spend, GpuError, GpuVerifier, Item};
 use super::ffi::{ZG_GEN_BINDING, ZG_GEN_SPEND_AUTH};
 use super::{ZG_KIND_OUTPUT, ZG_KIND_SPEND, ZG_KIND_SPROUT, ZG_STATUS_OK};
 
+#[derive(Clone)]
 pub struct JoinSplit {
     pub anchor: [u8; 32],
     pub random_seed: [u8; 32],
@@ -25,13 +35,17 @@ pub struct JoinSplit {
     pub commitments: [[u8; 32]; 2],
     pub vpub_old: u64,
     pub vpub_new: u64,
-    /// 192-byte Groth16 proof (v4+); None for a PGHR13 description (verdict in `pghr_ok`)
+    /// 192-byte Groth16 proof (v4+); None for a PGHR13 description
     pub groth_proof: Option<[u8; 192]>,
-    pub pghr_ok: bool,
+    /// 296-byte PHGR proof of a pre-Sapling description (verified in the window's PGHR13 call)
+    pub pghr_proof: Option<[u8; 296]>,
+    /// a PGHR13 verdict the caller already holds (overrides pghr_proof)
+    pub pghr_ok: Option<bool>,
     /// the caller's tree_cache.continue_root outcome (accept_transaction.rs:589)
     pub tree_error: Option<String>,
 }
 
+#[derive(Clone)]
 pub struct Spend {
     pub cv: [u8; 32],
     pub anchor: [u8; 32],
@@ -44,6 +58,7 @@ pub struct Spend {
     pub spend_auth_sig: Option<[u8; 64]>,
 }
 
+#[derive(Clone)]
 pub struct Output {
     pub cv: [u8; 32],
     pub cmu: [u8; 32],
@@ -51,7 +66,7 @@ pub struct Output {
     pub zkproof: [u8; 192],
 }
 
-#[derive(Default)]
+#[derive(Default, Clone)]
 pub struct Tx {
     /// first failing check before the JoinSplit stage (version ... eval)
     pub pre_error: Option<String>,
@@ -79,26 +94,63 @@ pub enum TxError {
     InvalidSapling,
 }
 
+/// What verifies a window: the GPU (`GpuVerifier`) or the reference's CPU calls (`CpuBackend`).
+pub trait Backend {
+    /// Groth16 statuses (ZG_STATUS_*), one per item, exact per proof
+    fn verify(&self, items: &[Item]) -> Result<Vec<u8>, GpuError>;
+    /// PGHR13 statuses for (296-byte proof, into_bn_frs inputs)
+    fn pghr13_verify(&self, items: &[([u8; 296], Vec<[u8; 32]>)]) -> Result<Vec<u8>, GpuError>;
+    /// RedJubjub verdicts for (vk, sig, msg, generator)
+    fn redjubjub_verify(&self, items: &[([u8; 32], [u8; 64], [u8; 64], u8)]) -> Result<Vec<bool>, GpuError>;
+    /// (status, bvk) per (spend cvs, output cvs, valueBalance)
+    fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError>;
+}
+
+impl Backend for GpuVerifier {
+    fn verify(&self, items: &[Item]) -> Result<Vec<u8>, GpuError> {
+        GpuVerifier::verify(self, items)
+    }
+    fn pghr13_verify(&self, items: &[([u8; 296], Vec<[u8; 32]>)]) -> Result<Vec<u8>, GpuError> {
+        GpuVerifier::pghr13_verify(self, items)
+    }
+    fn redjubjub_verify(&self, items: &[([u8; 32], [u8; 64], [u8; 64], u8)]) -> Result<Vec<bool>, GpuError> {
+        GpuVerifier::redjubjub_verify(self, items)
+    }
+    fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError> {
+        GpuVerifier::sapling_bvk(self, txs)
+    }
+}
+
 enum Plan {
     Proof(usize),
+    Pghr(usize),
     Caller(bool),
     Prep,
 }
 
-fn queue(txs: &[Tx]) -> (Vec<Item>, Vec<(Vec<Plan>, Vec<Plan>, Vec<Plan>)>) {
+type Plans = Vec<(Vec<Plan>, Vec<Plan>, Vec<Plan>)>;
+
+fn queue(txs: &[Tx]) -> (Vec<Item>, Vec<([u8; 296], Vec<[u8; 32]>)>, Plans) {
     let mut items = Vec::new();
+    let mut pghr = Vec::new();
     let mut plans = Vec::new();
     for tx in txs {
         let (mut js, mut sp, mut out) = (Vec::new(), Vec::new(), Vec::new());
         for d in &tx.joinsplits {
-            match (&d.groth_proof, &tx.js_pubkey) {
-                (Some(p), Some(pk)) => {
+            match (&d.groth_proof, &d.pghr_proof, d.pghr_ok, &tx.js_pubkey) {
+                (Some(p), _, _, Some(pk)) => {
                     let inputs = prep_joinsplit(&d.anchor, &d.random_seed, &d.nullifiers, &d.macs, &d.commitments,
                                                 d.vpub_old, d.vpub_new, pk);
                     js.push(Plan::Proof(items.len()));
                     items.push(Item { proof: *p, kind: ZG_KIND_SPROUT, inputs });
                 }
-                _ => js.push(Plan::Caller(d.pghr_ok)),
+                (None, Some(p), None, Some(pk)) => {
+                    let inputs = prep_joinsplit_bn(&d.anchor, &d.random_seed, &d.nullifiers, &d.macs,
+                                                   &d.commitments, d.vpub_old, d.vpub_new, pk);
+                    js.push(Plan::Pghr(pghr.len()));
+                    pghr.push((*p, inputs));
+                }
+                (_, _, v, _) => js.push(Plan::Caller(v.unwrap_or(false))),
             }
         }
         for s in &tx.spends {
@@ -121,12 +173,12 @@ fn queue(txs: &[Tx]) -> (Vec<Item>, Vec<(Vec<Plan>, Vec<Plan>, Vec<Plan>)>) {
         }
         plans.push((js, sp, out));
     }
-    (items, plans)
+    (items, pghr, plans)
 }
 
 /// (per-tx spend_auth verdicts, per-tx binding verdict): the GPU's for transactions with a
 /// sighash (one zg_sapling_bvk + one zg_redjubjub_verify call for the window), else the caller's
-fn sig_verdicts(v: &GpuVerifier, txs: &[Tx]) -> Result<(Vec<Vec<bool>>, Vec<bool>), GpuError> {
+fn sig_verdicts<B: Backend>(v: &B, txs: &[Tx]) -> Result<(Vec<Vec<bool>>, Vec<bool>), GpuError> {
     let mut sp: Vec<Vec<bool>> = txs.iter().map(|t| t.spends.iter().map(|s| s.sig_ok).collect()).collect();
     let mut bind: Vec<bool> = txs.iter().map(|t| t.binding_ok).collect();
     let need: Vec<usize> =
@@ -177,8 +229,8 @@ fn sig_verdicts(v: &GpuVerifier, txs: &[Tx]) -> Result<(Vec<Vec<bool>>, Vec<bool
     Ok((sp, bind))
 }
 
-fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8], sp_ok: &[bool], bind_ok: bool)
-            -> Option<TxError> {
+fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8], pghr_status: &[u8], sp_ok: &[bool],
+            bind_ok: bool) -> Option<TxError> {
     let (js, sp, out) = plan;
     if let Some(e) = &tx.pre_error {
         return Some(TxError::Caller(e.clone()));
@@ -190,6 +242,7 @@ fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8], sp
         for (i, (d, p)) in tx.joinsplits.iter().zip(js).enumerate() {
             let ok = match p {
                 Plan::Proof(k) => status[*k] == ZG_STATUS_OK,
+                Plan::Pghr(k) => pghr_status[*k] == ZG_STATUS_OK,
                 Plan::Caller(v) => *v,
                 Plan::Prep => false,
             };
@@ -235,16 +288,32 @@ fn tx_error(tx: &Tx, plan: &(Vec<Plan>, Vec<Plan>, Vec<Plan>), status: &[u8], sp
 
 /// Check the shielded proofs of a block (or an import window: transactions in chain order).
 /// Ok(None) if every transaction passes, else Ok(Some((tx_index, error))) with the error the
-/// reference reports; Err only for a GPU / runtime failure (the caller then falls back to
-/// the CPU path).
-pub fn verify_block(v: &GpuVerifier, txs: &[Tx]) -> Result<Option<(usize, TxError)>, GpuError> {
-    let (items, plans) = queue(txs);
+/// reference reports; Err only for a backend (GPU / runtime) failure.
+pub fn verify_block<B: Backend>(v: &B, txs: &[Tx]) -> Result<Option<(usize, TxError)>, GpuError> {
+    let (items, pghr, plans) = queue(txs);
     let status = if items.is_empty() { Vec::new() } else { v.verify(&items)? };
+    let pghr_status = if pghr.is_empty() { Vec::new() } else { v.pghr13_verify(&pghr)? };
     let (sp_ok, bind_ok) = sig_verdicts(v, txs)?;
     for (idx, (tx, plan)) in txs.iter().zip(&plans).enumerate() {
-        if let Some(e) = tx_error(tx, plan, &status, &sp_ok[idx], bind_ok[idx]) {
+        if let Some(e) = tx_error(tx, plan, &status, &pghr_status, &sp_ok[idx], bind_ok[idx]) {
             return Ok(Some((idx, e)));
         }
     }
     Ok(None)
+}
+
+/// The degradation path: the window on the GPU; on any GpuError (HIP error, lost device,
+/// ZG_E_DEBUG) the WHOLE window again on the reference's own CPU calls (`cpu::CpuBackend`:
+/// verify_proof, pghr13_verify, redjubjub), which cannot fail this way. The window's
+/// statuses never mix the two backends. `on_gpu_error` is told what failed (log it, and stop
+/// using the device if it keeps failing).
+pub fn verify_block_or_cpu(gpu: Option<&GpuVerifier>, cpu: &CpuBackend, txs: &[Tx],
+                           on_gpu_error: &dyn Fn(&GpuError)) -> Option<(usize, TxError)> {
+    if let Some(g) = gpu {
+        match verify_block(g, txs) {
+            Ok(r) => return r,
+            Err(e) => on_gpu_error(&e),
+        }
+    }
+    verify_block(cpu, txs).expect("the CPU backend does not fail")
 }

@@ -40,6 +40,7 @@ pub const ZG_E_VK: c_int = -4;
 pub const ZG_E_NOMEM: c_int = -5;
 pub const ZG_E_STATE: c_int = -6;
 pub const ZG_E_TREE_FULL: c_int = -7;
+pub const ZG_E_DEBUG: c_int = -8;
 
 pub const ZG_PROOF_BYTES: usize = 192;
 pub const ZG_FR_BYTES: usize = 32;
@@ -99,6 +100,9 @@ extern "C" {
     pub fn zg_prep_joinsplit(anchor: *const u8, random_seed: *const u8, nullifiers: *const u8, macs: *const u8,
                              commitments: *const u8, vpub_old: u64, vpub_new: u64, pubkey: *const u8,
                              inputs: *mut u8) -> c_int;
+    pub fn zg_prep_joinsplit_bn(anchor: *const u8, random_seed: *const u8, nullifiers: *const u8, macs: *const u8,
+                                commitments: *const u8, vpub_old: u64, vpub_new: u64, pubkey: *const u8,
+                                inputs: *mut u8) -> c_int;
     pub fn zg_hsig(random_seed: *const u8, nf0: *const u8, nf1: *const u8, pubkey: *const u8, out: *mut u8) -> c_int;
 
     pub fn zg_redjubjub_verify(ctx: *mut ZgCtx, n: usize, vk: *const u8, sig: *const u8, msg: *const u8,
@@ -134,4 +138,6 @@ extern "C" {
                               out: *mut u8) -> c_int;
     pub fn zg_bench_mad_rate(ctx: *mut ZgCtx, macs_per_s: *mut f64) -> c_int;
     pub fn zg_bench_mad_rate_clock(ctx: *mut ZgCtx, macs_per_s: *mut f64, clock_hz: *mut f64) -> c_int;
+    pub fn zg_debug_field_mul(device: c_int, field: c_int, n: usize, a: *const u8, b: *const u8, out: *mut u8)
+                              -> c_int;
 }

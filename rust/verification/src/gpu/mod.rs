@@ -8,7 +8,9 @@
 //! zebra_amd/collector.py, which tests/test_collector.py checks against the reference's real
 //! transactions).
 pub mod collect;
+pub mod cpu;
 pub mod ffi;
+pub mod writer;
 
 use std::ffi::CStr;
 use std::os::raw::c_int;
@@ -167,6 +169,32 @@ impl GpuVerifier {
         Ok(ok.into_iter().map(|b| b == 1).collect())
     }
 
+    /// PHGR JoinSplit proofs (sprout.rs:61-67): per item the 296-byte proof and its
+    /// into_bn_frs inputs (`prep_joinsplit_bn`) -> ZG_STATUS_* (DECODE_INVALID = InvalidEncoding,
+    /// VERIFY_FAILED = InvalidPGHRProof). The builtin res/sprout-verifying-key.json is loaded on
+    /// first use.
+    pub fn pghr13_verify(&self, items: &[([u8; 296], Vec<[u8; 32]>)]) -> Result<Vec<u8>, GpuError> {
+        let _g = self.lock.lock().unwrap();
+        let n = items.len();
+        let mut proofs = Vec::with_capacity(296 * n);
+        let mut inputs = vec![0u8; ffi::ZG_INPUT_STRIDE * n];
+        let mut counts = Vec::with_capacity(n);
+        for (i, (p, x)) in items.iter().enumerate() {
+            proofs.extend_from_slice(p);
+            counts.push(x.len().min(ffi::ZG_MAX_INPUTS) as u8);
+            for (j, v) in x.iter().enumerate().take(ffi::ZG_MAX_INPUTS) {
+                let o = ffi::ZG_INPUT_STRIDE * i + ffi::ZG_FR_BYTES * j;
+                inputs[o..o + ffi::ZG_FR_BYTES].copy_from_slice(v);
+            }
+        }
+        let mut status = vec![0u8; n];
+        check(self.ctx, unsafe {
+            ffi::zg_pghr13_verify(self.ctx, n, proofs.as_ptr(), inputs.as_ptr(), counts.as_ptr(), status.as_mut_ptr(),
+                                  std::ptr::null_mut())
+        })?;
+        Ok(status)
+    }
+
     /// binding verification keys: per tx (spend cvs, output cvs, valueBalance) -> (status, bvk)
     pub fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError> {
         let _g = self.lock.lock().unwrap();
@@ -238,10 +266,12 @@ pub fn prep_output(cv: &[u8; 32], cmu: &[u8; 32], epk: &[u8; 32]) -> Result<Vec<
     Ok(out.chunks(32).map(|c| c.try_into().unwrap()).collect())
 }
 
-/// sprout::verify's input (sprout.rs:34-58,86-153) -> 9 Fr
+/// sprout::verify's input (sprout.rs:34-58,86-153) -> 9 BLS12-381 Fr (into_bls_frs, the
+/// Groth16 branch); `bn = true`: the same bits as 9 BN254 Fr (into_bn_frs, the PHGR branch)
 #[allow(clippy::too_many_arguments)]
-pub fn prep_joinsplit(anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[u8; 32]; 2], macs: &[[u8; 32]; 2],
-                      commitments: &[[u8; 32]; 2], vpub_old: u64, vpub_new: u64, pubkey: &[u8; 32]) -> Vec<[u8; 32]> {
+fn prep_joinsplit_any(bn: bool, anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[u8; 32]; 2],
+                      macs: &[[u8; 32]; 2], commitments: &[[u8; 32]; 2], vpub_old: u64, vpub_new: u64,
+                      pubkey: &[u8; 32]) -> Vec<[u8; 32]> {
     let cat = |x: &[[u8; 32]; 2]| -> [u8; 64] {
         let mut o = [0u8; 64];
         o[..32].copy_from_slice(&x[0]);
@@ -251,8 +281,25 @@ pub fn prep_joinsplit(anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[
     let (nf, mc, cm) = (cat(nullifiers), cat(macs), cat(commitments));
     let mut out = [0u8; 9 * 32];
     unsafe {
-        ffi::zg_prep_joinsplit(anchor.as_ptr(), random_seed.as_ptr(), nf.as_ptr(), mc.as_ptr(), cm.as_ptr(), vpub_old,
-                               vpub_new, pubkey.as_ptr(), out.as_mut_ptr());
+        if bn {
+            ffi::zg_prep_joinsplit_bn(anchor.as_ptr(), random_seed.as_ptr(), nf.as_ptr(), mc.as_ptr(), cm.as_ptr(),
+                                      vpub_old, vpub_new, pubkey.as_ptr(), out.as_mut_ptr());
+        } else {
+            ffi::zg_prep_joinsplit(anchor.as_ptr(), random_seed.as_ptr(), nf.as_ptr(), mc.as_ptr(), cm.as_ptr(),
+                                   vpub_old, vpub_new, pubkey.as_ptr(), out.as_mut_ptr());
+        }
     }
     out.chunks(32).map(|c| c.try_into().unwrap()).collect()
+}
+
+#[allow(clippy::too_many_arguments)]
+pub fn prep_joinsplit(anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[u8; 32]; 2], macs: &[[u8; 32]; 2],
+                      commitments: &[[u8; 32]; 2], vpub_old: u64, vpub_new: u64, pubkey: &[u8; 32]) -> Vec<[u8; 32]> {
+    prep_joinsplit_any(false, anchor, random_seed, nullifiers, macs, commitments, vpub_old, vpub_new, pubkey)
+}
+
+#[allow(clippy::too_many_arguments)]
+pub fn prep_joinsplit_bn(anchor: &[u8; 32], random_seed: &[u8; 32], nullifiers: &[[u8; 32]; 2], macs: &[[u8; 32]; 2],
+                         commitments: &[[u8; 32]; 2], vpub_old: u64, vpub_new: u64, pubkey: &[u8; 32]) -> Vec<[u8; 32]> {
+    prep_joinsplit_any(true, anchor, random_seed, nullifiers, macs, commitments, vpub_old, vpub_new, pubkey)
 }

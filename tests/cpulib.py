@@ -65,3 +65,43 @@ def merkle_window(L, kind, height, state, leaves, marks):
     out = ctypes.create_string_buffer(max(32 * nm, 1))
     rc = L.mc_window(kind, height, bytes(state), len(state), len(leaves), b"".join(leaves), nm, mk, out)
     return rc, [out.raw[32 * k:32 * k + 32] for k in range(nm)]
+
+
+def load_pghr13():
+    """oracle/_build/libpghr13cpu.so (pghr13_cpu.cpp, the reference's PGHR13 check restated in
+    C++), with the key of res/sprout-verifying-key.json (parsed and point-checked by
+    oracle.pghr13.load_vk_json)"""
+    from oracle import pghr13 as PG
+    lib = runpy.run_path(os.path.join(ROOT, "oracle", "cpu", "build.py"))["build_pghr13"]()
+    L = ctypes.CDLL(lib)
+    L.pg_vk_load.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.pg_pairing.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    L.pg_verify.argtypes = [ctypes.c_size_t] + [ctypes.c_char_p] * 4 + [ctypes.c_int]
+    vk = PG.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res", "sprout-verifying-key.json")).read())
+    le = lambda x: x.to_bytes(32, "little")  # noqa: E731
+    g1 = lambda p: le(p[0]) + le(p[1])  # noqa: E731
+    g2 = lambda q: le(q[0][0]) + le(q[0][1]) + le(q[1][0]) + le(q[1][1])  # noqa: E731
+    blob = b"".join(g2(vk[k]) for k in ("a", "c", "z", "gamma", "gamma_beta_2"))
+    blob += g1(vk["b"]) + g1(vk["gamma_beta_1"]) + b"".join(g1(p) for p in vk["ic"])
+    assert L.pg_vk_load(blob, len(vk["ic"])) == 0
+    return L
+
+
+def pg_verify(L, proofs, inputs, threads=1):
+    """proofs: 296-byte PHGR proofs; inputs: per proof a list of <= 9 32-byte LE BN254 Fr"""
+    n = len(proofs)
+    rows = b"".join(b"".join(bytes(x) for x in r) + bytes(32 * (9 - len(r))) for r in inputs)
+    st = ctypes.create_string_buffer(max(n, 1))
+    assert L.pg_verify(n, b"".join(map(bytes, proofs)), rows, bytes(len(r) for r in inputs), st, threads) == 0
+    return list(st.raw[:n])
+
+
+def pg_pairing(L, ps, qs):
+    """e(P, Q) per pair (affine integer points) -> GT as 12 integers (oracle.bn254.gt_ints order)"""
+    le = lambda x: x.to_bytes(32, "little")  # noqa: E731
+    g1 = b"".join(le(p[0]) + le(p[1]) for p in ps)
+    g2 = b"".join(le(q[0][0]) + le(q[0][1]) + le(q[1][0]) + le(q[1][1]) for q in qs)
+    out = ctypes.create_string_buffer(384 * len(ps))
+    L.pg_pairing(len(ps), g1, g2, out)
+    return [[int.from_bytes(out.raw[384 * i + 32 * k:384 * i + 32 * k + 32], "little") for k in range(12)]
+            for i in range(len(ps))]

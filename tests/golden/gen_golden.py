@@ -670,6 +670,46 @@ def gen_pghr13():
     print("wrote pghr13.json", len(cases), "cases")
 
 
+def gen_pghr13_descs():
+    """adds "joinsplit_txs" to pghr13.json: the transactions of test-data blocks 522 and 567 that
+    carry PHGR JoinSplits (test-data/src/lib.rs:97-110), as description fields (anchor, random
+    seed, nullifiers, macs, commitments, vpub_old / vpub_new, the 296-byte proof) with the
+    transaction's JoinSplit pubkey -- what a block-level caller hands the collector, which then
+    derives the BN inputs itself. Each description's packed inputs are asserted equal to the
+    matching h522 / h567 case already in the file; no verdict is recomputed."""
+    from oracle import pghr13 as PG
+    path = os.path.join(HERE, "pghr13.json")
+    data = json.load(open(path))
+    by_name = {c["name"]: c for c in data["cases"]}
+    lib = open(os.path.join(REF, "test-data/src/lib.rs")).read()
+    out = []
+    for fn in ("pub fn block_h522()", "pub fn block_h567()"):
+        seg = lib[lib.index(fn):]
+        hx_ = re.search(r'"([0-9a-f]{200,})"', seg[:seg.index("\n}\n")]).group(1)
+        _, txs = Z.parse_block_hex(hx_)
+        k = 0
+        blk = fn.split("_")[1][:-2]
+        for t in txs:
+            descs = []
+            for d in t["joinsplits"]:
+                if d["groth"]:
+                    continue
+                name = "%s_tx%s_js%d" % (blk, t["txid"][:8], k)
+                k += 1
+                ins = [x.to_bytes(32, "little").hex() for x in PG.joinsplit_inputs(d, t["js_pubkey"])]
+                assert ins == by_name[name]["inputs"] and d["zkproof"].hex() == by_name[name]["proof"], name
+                descs.append({"case": name, "anchor": d["anchor"].hex(), "random_seed": d["random_seed"].hex(),
+                              "nullifiers": [x.hex() for x in d["nullifiers"]], "macs": [x.hex() for x in d["macs"]],
+                              "commitments": [x.hex() for x in d["commitments"]], "vpub_old": d["vpub_old"],
+                              "vpub_new": d["vpub_new"], "zkproof": d["zkproof"].hex()})
+            if descs:
+                out.append({"block": blk, "txid": t["txid"], "js_pubkey": t["js_pubkey"].hex(), "joinsplits": descs})
+    data["joinsplit_txs"] = out
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print("added", len(out), "PHGR transactions to pghr13.json")
+
+
 def refresh_batch_gt():
     """recompute batch64.json's gt_out from its stored per-proof lhs_gt and r bytes (after a
     change of the batch-scalar mapping; no reference sources needed)"""
@@ -697,6 +737,8 @@ if __name__ == "__main__":
         gen_sapling_sigs()
     elif len(sys.argv) > 1 and sys.argv[1] == "--pghr13":
         gen_pghr13()
+    elif len(sys.argv) > 1 and sys.argv[1] == "--pghr13-descs":
+        gen_pghr13_descs()
     elif len(sys.argv) > 1 and sys.argv[1] == "--tree-state":
         gen_tree_state()
     else:

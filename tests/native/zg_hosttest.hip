@@ -14,6 +14,17 @@ static void st_fq(const Fq& a, uint8_t* b) { fq_limbs_to_be(fq_from_mont(a), b);
 
 extern "C" {
 
+// the products of zg_debug_field_mul (zebra_amd/csrc/zg_debug.hip) on the host: same field ids
+void zgt_field_mul(int field, const uint32_t* a, const uint32_t* b, uint32_t* r) {
+  switch (field) {
+    case 0: fq29_mul(r, a, b); break;
+    case 1: fq29_sqr(r, a); break;
+    case 2: f2_mul29(r, r + 12, a, a + 12, b, b + 12); break;
+    case 3: fr29_mul(r, a, b); break;
+    default: bq29_mul(r, a, b); break;
+  }
+}
+
 void zgt_fq_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_mul(ld_fq(a), ld_fq(b)), out); }
 void zgt_fq_add(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_add(ld_fq(a), ld_fq(b)), out); }
 void zgt_fq_sub(const uint8_t* a, const uint8_t* b, uint8_t* out) { st_fq(fq_sub(ld_fq(a), ld_fq(b)), out); }

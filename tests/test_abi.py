@@ -29,6 +29,8 @@ def test_library_exports_all_declared_symbols():
     assert not missing, missing
     L.zg_version.restype = ctypes.c_char_p
     assert b"gfx950" in L.zg_version()
+    # build provenance: the library reports the hash of the sources it was compiled from
+    assert L.zg_version().decode().endswith(" src " + build.source_hash())
 
 
 def test_code_object_targets_gfx950():

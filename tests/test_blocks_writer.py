@@ -135,3 +135,44 @@ def test_deferred_writer_on_gpu():
         assert got == want and got[1] is not None and got[0][-1] == "b27"
     finally:
         ctx.close()
+
+
+def fork_stream(n, seed, F, bad_proof=(), bad_pre=()):
+    """a main chain b1..bn plus sibling fork blocks f<i> (parent b<i>) and a fork child f<i>c,
+    delivered a few blocks after their parent; failures on main or fork blocks"""
+    from zebra_amd.blocks_writer import Block
+    rng = random.Random(seed)
+    names = list(SRC_TX.values())
+    main = chain(n, seed, F, bad_proof=bad_proof, bad_pre=bad_pre)
+    out = list(main)
+    for i in sorted(rng.sample(range(1, n - 2), 3)):
+        txs = [make_tx(rng.choice(names), F) for _ in range(rng.randint(1, 2))]
+        if ("f%d" % i) in bad_proof:
+            txs[0].outputs.append(make_tx(["O1"], F).outputs[0])
+            c = bytearray(txs[0].outputs[-1].zkproof)
+            c[10] ^= 1
+            txs[0].outputs[-1].zkproof = bytes(c)
+        fb = Block("f%d" % i, "b%d" % i, txs)
+        fc = Block("f%dc" % i, "f%d" % i, [make_tx(rng.choice(names), F)])
+        at = out.index(main[min(n - 1, i + 1)]) + 1
+        out[at:at] = [fb, fc]
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_deferred_equals_sequential_with_forks(cpu_verify, seed):
+    """sibling forks in the stream: identical storage order and first error, with
+    the failure on the main chain, on a fork block, or nowhere"""
+    from zebra_amd.blocks_writer import DeferredBlocksWriter, SequentialBlocksWriter
+    F = fields()
+    rng = random.Random(300 + seed)
+    n = 16
+    bad = {0: (), 1: {rng.randrange(n)}, 2: set(), 3: {rng.randrange(n)}}[seed]
+    stream = fork_stream(n, seed, F, bad_proof=bad)
+    if seed == 2:   # a failing fork block
+        stream = fork_stream(n, seed, F, bad_proof={"f%d" % int(b.hash[1:]) for b in stream
+                                                   if b.hash.startswith("f") and not b.hash.endswith("c")})
+    want = run(SequentialBlocksWriter, stream, **seq_kw(cpu_verify))
+    assert any(h.startswith("f") for h in want[0]) or want[1] is not None
+    for window in (1, 5, 10 ** 6):
+        assert run(DeferredBlocksWriter, stream, **deferred_kw(cpu_verify, window)) == want, (seed, window)

@@ -260,3 +260,115 @@ def test_signatures_in_reference_order_gpu():
         _sig_cases(lambda txs: verify_block(txs, ctx=ctx))
     finally:
         ctx.close()
+
+
+# ---- PHGR (PGHR13) JoinSplits in the window: mainnet block 522 (tests/golden/pghr13.json)
+def pghr_txs():
+    """block 522's five transactions with PHGR JoinSplits (one carries two), as the collector's
+    Tx view; the BN inputs are derived by the collector (zg_prep_joinsplit_bn)"""
+    from zebra_amd.collector import JoinSplit, Tx
+    out = []
+    for t in load_golden("pghr13.json")["joinsplit_txs"]:
+        tx = Tx(js_pubkey=h(t["js_pubkey"]))
+        for d in t["joinsplits"]:
+            tx.joinsplits.append(JoinSplit(h(d["anchor"]), h(d["random_seed"]), [h(x) for x in d["nullifiers"]],
+                                           [h(x) for x in d["macs"]], [h(x) for x in d["commitments"]],
+                                           d["vpub_old"], d["vpub_new"], h(d["zkproof"]), groth=False))
+        out.append(tx)
+    return out
+
+
+def test_prep_joinsplit_bn_matches_block_522():
+    """zg_prep_joinsplit_bn (into_bn_frs, 253-bit chunks) reproduces the inputs of the block-522
+    PHGR cases; the BLS packing of the same bits differs (254-bit chunks)"""
+    from zebra_amd import zg
+    cases = {c["name"]: c for c in load_golden("pghr13.json")["cases"]}
+    n = 0
+    for t in load_golden("pghr13.json")["joinsplit_txs"]:
+        for d in t["joinsplits"]:
+            args = (h(d["anchor"]), h(d["random_seed"]), [h(x) for x in d["nullifiers"]], [h(x) for x in d["macs"]],
+                    [h(x) for x in d["commitments"]], d["vpub_old"], d["vpub_new"], h(t["js_pubkey"]))
+            got = zg.prep_joinsplit_bn(*args)
+            assert [g.hex() for g in got] == cases[d["case"]]["inputs"], d["case"]
+            assert zg.prep_joinsplit(*args) != got
+            n += 1
+    assert n == 6
+
+
+def _corrupt_sign(proof):
+    b = bytearray(proof)
+    b[0] ^= 1                   # a's y-parity flag: decodes, fails verification (InvalidPGHRProof)
+    return bytes(b)
+
+
+def _corrupt_prefix(proof):
+    b = bytearray(proof)
+    b[66] = 2                   # b's G2 prefix: from_raw fails (InvalidEncoding)
+    return bytes(b)
+
+
+def _pghr_cases(run, groth_txs):
+    """PHGR descriptions in reference precedence, mixed with Groth16 transactions"""
+    txs = groth_txs() + pghr_txs()
+    base = len(txs) - 5
+    assert run(txs) is None
+    txs = groth_txs() + pghr_txs()
+    js = txs[base + 4].joinsplits                    # the transaction with two PHGR JoinSplits
+    js[1].zkproof = _corrupt_sign(js[1].zkproof)
+    assert run(txs) == (base + 4, ("InvalidJoinSplit", 1))
+    js[0].tree_error = "UnknownAnchor"               # description 0 passes its proof, then its root fails
+    assert run(txs) == (base + 4, "UnknownAnchor")
+    js[0].zkproof = _corrupt_prefix(js[0].zkproof)   # now description 0's proof fails first
+    assert run(txs) == (base + 4, ("InvalidJoinSplit", 0))
+    txs[base + 1].joinsplits[0].zkproof = _corrupt_prefix(txs[base + 1].joinsplits[0].zkproof)
+    assert run(txs) == (base + 1, ("InvalidJoinSplit", 0))   # the lowest failing transaction wins
+    s = txs[1].spends[0] if txs[1].spends else None
+    if s is not None:
+        s.nullifier = bytes(32)                      # an earlier Groth16 failure wins over both
+        assert run(txs) == (1, "InvalidSapling")
+    txs = groth_txs() + pghr_txs()
+    txs[base + 2].joinsplits[0].pghr_ok = False      # a verdict the caller already holds
+    assert run(txs) == (base + 2, ("InvalidJoinSplit", 0))
+
+
+def _groth_txs():
+    F = fields()
+    return [make_tx(SRC_TX[k], F) for k in ("smoky", "bd4fe81c", "991edf59")]
+
+
+def test_pghr_joinsplits_in_reference_order_cpu(cpu_verify):
+    """the collector's PHGR queue and precedence with the oracle's PGHR13 verifier (checker only;
+    known fixture statements answered from their pinned statuses, mutants verified by the oracle)"""
+    from oracle import pghr13 as PG
+    from zebra_amd.collector import verify_block
+    known = {(c["proof"], tuple(c["inputs"])): c["status"] for c in load_golden("pghr13.json")["cases"]}
+    vk = []
+
+    def verify_pghr(proofs, inputs):
+        out = []
+        for p, x in zip(proofs, inputs):
+            k = (bytes(p).hex(), tuple(bytes(v).hex() for v in x))
+            if k not in known:
+                if not vk:
+                    import os
+                    from tests.conftest import ROOT
+                    vk.append(PG.load_vk_json(open(os.path.join(ROOT, "zebra_amd", "res",
+                                                                "sprout-verifying-key.json")).read()))
+                known[k] = PG.verify_raw(vk[0], bytes(p), [int.from_bytes(bytes(v), "little") for v in x])
+            out.append(known[k])
+        return out
+    _pghr_cases(lambda txs: verify_block(txs, verify=cpu_verify, verify_pghr=verify_pghr), _groth_txs)
+
+
+@pytest.mark.gpu
+def test_pghr_joinsplits_block_522_gpu():
+    """block 522's six PHGR JoinSplits mixed with Groth16 transactions through verify_block on the
+    product: one zg_verify_batch + one zg_pghr13_verify per window; corrupted PHGR proofs surface
+    as InvalidJoinSplit(index) on the right transaction (accept_transaction.rs:575-592)"""
+    from zebra_amd import Context
+    from zebra_amd.collector import verify_block
+    ctx = Context(device=0, max_batch=64)
+    try:
+        _pghr_cases(lambda txs: verify_block(txs, ctx=ctx), _groth_txs)
+    finally:
+        ctx.close()

@@ -28,8 +28,12 @@ def fx_batch(items):
 
 
 def test_library_is_gfx950_hip():
-    from zebra_amd import zg
-    assert b"gfx950" in zg.lib().zg_version()
+    """the loaded library is the gfx950 build of exactly the sources in this tree (zg_version
+    carries their hash, zebra_amd/build.py source_hash)"""
+    from zebra_amd import build, zg
+    v = zg.lib().zg_version().decode()
+    assert "gfx950" in v
+    assert v.endswith(" src " + build.source_hash()), (v, build.source_hash())
 
 
 def test_mad_rate_probe(ctx):
@@ -249,3 +253,32 @@ def test_many_slots_in_flight():
     finally:
         for c in cs:
             c.close()
+
+
+def test_debug_each_cross_check():
+    """ZG_DEBUG_EACH=1 (debug mode): every batch's statuses are re-checked on the
+    device by the per-proof verify_proof kernel; a clean and a corrupted batch pass the check
+    (no ZG_E_DEBUG) and keep the oracle's reject set"""
+    import os
+    from tests import cpulib
+    from tests.test_gpu_configs import SRCS, _sources, config3_indices, corrupt, oracle_statuses
+    from zebra_amd import Context, pack_inputs
+    _, src_proofs, src_kinds, rows = _sources()
+    n = 512
+    idx = config3_indices(n)
+    os.environ["ZG_DEBUG_EACH"] = "1"
+    try:
+        c = Context(device=0, max_batch=n)
+    finally:
+        del os.environ["ZG_DEBUG_EACH"]
+    try:
+        proofs = c.synth_rerandomize(src_proofs, src_kinds, idx, 5)
+        kinds = bytes(src_kinds[j] for j in idx)
+        inputs = pack_inputs([rows[SRCS[j]] for j in idx])
+        assert c.verify_batch(proofs, kinds, inputs)[0] == [0] * n
+        bp, bx, bad = corrupt(proofs, kinds, inputs, 12, 3)
+        want = oracle_statuses(cpulib.load(), bp, kinds, bx, bad)
+        sts, _ = c.verify_batch(bp, kinds, bx)
+        assert {i: s for i, s in enumerate(sts) if s} == want
+    finally:
+        c.close()

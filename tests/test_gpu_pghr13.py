@@ -93,3 +93,41 @@ def test_gpu_pghr13_vk_checks(ctx):
     ctx.pghr13_vk_load_json(json.dumps(d))
     c = GOLDEN["cases"][0]
     assert ctx.pghr13_verify([bytes.fromhex(c["proof"])], [_inputs(c)]) == [c["status"]]
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_keys_per_context():
+    """keys belong to the context that loaded them: two fresh contexts verifying
+    concurrently on first use both get the builtin key; a different valid key loaded on one
+    context changes only that context's verdicts; a failed load leaves its key unchanged"""
+    import threading
+    from zebra_amd import Context, zg
+    valid = [c for c in GOLDEN["cases"] if c["status"] == 0]
+    proofs = [bytes.fromhex(c["proof"]) for c in valid] * 8
+    inputs = [_inputs(c) for c in valid] * 8
+    a, b = Context(device=0, max_batch=64, load_builtin=False), Context(device=0, max_batch=64, load_builtin=False)
+    try:
+        res = {}
+        ts = [threading.Thread(target=lambda k=k, c=c: res.__setitem__(k, c.pghr13_verify(proofs, inputs)))
+              for k, c in (("a", a), ("b", b))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert res == {"a": [0] * len(proofs), "b": [0] * len(proofs)}
+        d = json.load(open(os.path.join(ROOT, "zebra_amd", "res", "sprout-verifying-key.json")))
+        other = dict(d)
+        other["ic"] = d["ic"][2:4] + d["ic"][0:2] + d["ic"][4:]   # ic[0] <-> ic[1]: a valid, different key
+        a.pghr13_vk_load_json(json.dumps(other))
+        assert a.pghr13_verify(proofs, inputs) == [zg.STATUS_VERIFY_FAILED] * len(proofs)
+        assert b.pghr13_verify(proofs, inputs) == [0] * len(proofs)
+        bad = dict(d)
+        bad["alphaB"] = [d["alphaB"][0], d["alphaB"][0]]
+        with pytest.raises(zg.ZgError):
+            a.pghr13_vk_load_json(json.dumps(bad))
+        assert a.pghr13_verify(proofs[:2], inputs[:2]) == [zg.STATUS_VERIFY_FAILED] * 2   # still `other`
+        a.pghr13_vk_load_builtin()
+        assert a.pghr13_verify(proofs, inputs) == [0] * len(proofs)
+    finally:
+        a.close()
+        b.close()

@@ -186,3 +186,30 @@ def test_batch_scalar_glv(L):
         L.zgt_g1_glv_mul(fq_b(p[0]) + fq_b(p[1]), r16, out)
         q = B.ec_mul(B.FQ, p, r)
         assert (int.from_bytes(out.raw[:48], "big"), int.from_bytes(out.raw[48:], "big")) == q
+
+
+@pytest.mark.parametrize("field", [0, 1, 2, 3, 4])
+def test_field_products_host_edges(L, field):
+    """the operand sets of tests/test_gpu_field.py through the same generated products on the
+    host (zgt_field_mul == zg_debug_field_mul's switch): pins the expected values the GPU test
+    asserts, and the generated C itself on its edge operands"""
+    import ctypes
+    from tests import test_gpu_field as TF
+    fn = L.zgt_field_mul
+    fn.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    if field == 2:
+        pairs = TF.fq2_cases()[:1500]
+        for x, y in pairs:
+            out = ctypes.create_string_buffer(96)
+            fn(2, TF.fq2_enc(x), TF.fq2_enc(y), out)
+            assert (int.from_bytes(out.raw[:48], "little"), int.from_bytes(out.raw[48:], "little")) == \
+                TF.fq2_expected(x, y)
+        return
+    w = TF.FIELDS[field][2]
+    pairs = TF.cases(field)[:3000]
+    got = []
+    for x, y in pairs:
+        out = ctypes.create_string_buffer(w)
+        fn(field, x.to_bytes(w, "little"), y.to_bytes(w, "little"), out)
+        got.append(out.raw)
+    assert not TF.mismatches(field, pairs, got)

@@ -238,3 +238,38 @@ def test_deferred_verdicts_world2():
         # without waiting for batch 0's verdict (the worker thread logs verdicts concurrently)
         main = [e for e in log if e[0] != "verdict"]
         assert main.index(("launch", 3)) == main.index(("harvest", 0)) + 1
+
+
+def _multi_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from zebra_amd.dist import combine_partials
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = [bytes([16 * rank + j]) * 576 for j in range(3)]
+        seen = []
+        ok = combine_partials(mine, lambda parts: seen.extend(parts) or True, world, rank, "cpu")
+        q.put((rank, ok, [p[0] for p in seen]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_several_shards_each():
+    """a rank holding k shards sends its k partials in the same single all-gather; every rank
+    sees all world x k of them, rank-major (the order of the contiguous shards)"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs)
+    for _, ok, order in res:
+        assert ok and order == [0, 1, 2, 16, 17, 18]

@@ -19,6 +19,14 @@ the sequential writer would never have inserted them.
 
 Error precedence inside a block is the collector's (accept_transaction.rs:68-84,
 accept_chain.rs:76-81: the lowest failing transaction wins); across blocks the lowest block wins.
+
+Contract: the equivalence holds for a caller that stops at the first error, as the reference's
+only caller does (zebra/commands/import.rs:20-28 returns on any Err from append_block). The
+error of a block surfaces when its window is verified -- at that block's append_block or at a
+later append_block / flush -- and the window's blocks after the failing one are dropped,
+including blocks on a sibling fork that the sequential writer would have inserted had the caller
+kept appending after the error. Forks inside a window are otherwise handled like the sequential
+writer (tests/test_blocks_writer.py: sibling forks with and without failures).
 """
 from collections import OrderedDict
 

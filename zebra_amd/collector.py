@@ -17,11 +17,15 @@ reference's:
       per output (cv, cmu, epk, proof), binding signature -> any failure is InvalidSapling;
       then Sapling nullifiers
 
-The checks that are not Groth16 (signatures, tree roots, nullifiers, the transparent
-checks before the shielded stages, PGHR13 proofs of pre-Sapling JoinSplits) are evaluated by
-the caller exactly as today and handed in as outcomes; the collector prepares every Groth16
-public input with the product's host code (zg_prep_*), verifies all proofs of the block in
-one zg_verify_batch call and re-injects the per-proof statuses in reference order.
+The checks that are not proofs or Sapling signatures (JoinSplit ed25519 signature, tree
+roots, nullifiers, the transparent checks before the shielded stages) are evaluated by the
+caller exactly as today and handed in as outcomes; the collector prepares every Groth16 public
+input with the product's host code (zg_prep_*), verifies all Groth16 proofs of the window in
+one zg_verify_batch call and all PGHR13 proofs of pre-Sapling JoinSplits (sprout.rs:61-67,
+inputs Input::into_bn_frs via zg_prep_joinsplit_bn) in one zg_pghr13_verify call, and
+re-injects the per-proof statuses in reference order: a PHGR description that fails to decode
+(InvalidEncoding) or to verify (InvalidPGHRProof) is InvalidJoinSplit(index), at its place among
+the transaction's descriptions, before its tree_cache.continue_root (accept_transaction.rs:575-592).
 """
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -43,7 +47,8 @@ class JoinSplit:
     vpub_new: int
     zkproof: bytes                    # 192 B Groth16 (v4+) or 296 B PGHR13
     groth: bool = True
-    pghr_ok: Optional[bool] = None    # caller's PGHR13 verdict for a non-Groth description
+    pghr_ok: Optional[bool] = None    # a PGHR13 verdict the caller already holds (None: the GPU
+                                      # verifies the description in the window's PGHR13 call)
     tree_error: Optional[str] = None  # caller's tree_cache.continue_root outcome (None = ok)
 
 
@@ -86,14 +91,20 @@ class Tx:
 
 
 def _queue(txs):
-    """prepare inputs; returns (items, per-tx plans). A plan entry refers to a queued proof by
-    index, or carries a prep error."""
-    items, plans = [], []
+    """prepare inputs; returns (Groth16 items, PGHR13 items, per-tx plans). A plan entry refers
+    to a queued proof by index ("proof" / "pghr"), or carries a prep error or a caller verdict."""
+    items, pghr, plans = [], [], []
     for tx in txs:
         js_plan, sp_plan, out_plan = [], [], []
         for d in tx.joinsplits:
-            if not d.groth or tx.js_pubkey is None:
+            if tx.js_pubkey is None or (not d.groth and d.pghr_ok is not None):
                 js_plan.append(("caller", bool(d.pghr_ok)))
+                continue
+            if not d.groth:
+                inp = zg.prep_joinsplit_bn(d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments,
+                                           d.vpub_old, d.vpub_new, tx.js_pubkey)
+                js_plan.append(("pghr", len(pghr)))
+                pghr.append((bytes(d.zkproof), inp))
                 continue
             inp = zg.prep_joinsplit(d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old,
                                     d.vpub_new, tx.js_pubkey)
@@ -116,7 +127,7 @@ def _queue(txs):
             out_plan.append(("proof", len(items)))
             items.append((zg.KIND_OUTPUT, bytes(o.zkproof), inp))
         plans.append((js_plan, sp_plan, out_plan))
-    return items, plans
+    return items, pghr, plans
 
 
 def _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk):
@@ -133,6 +144,9 @@ def _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk):
     need = [i for i, tx in enumerate(txs) if tx.sighash is not None and (tx.spends or tx.outputs)]
     if not need:
         return sp_ok, bind_ok
+    if verify_sigs is None or sapling_bvk is None:
+        raise zg.ZgError(-1, "transactions carry a sighash but no signature backend was given "
+                             "(pass ctx=, or verify_sigs= and sapling_bvk=)")
     bvks = sapling_bvk([([s.cv for s in txs[i].spends], [o.cv for o in txs[i].outputs], txs[i].value_balance)
                         for i in need])
     items, where = [], []
@@ -158,7 +172,7 @@ def _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk):
     return sp_ok, bind_ok
 
 
-def _tx_error(tx, plan, status, sp_ok=None, bind_ok=None):
+def _tx_error(tx, plan, status, sp_ok=None, bind_ok=None, pghr_status=()):
     """the reference's first error of one transaction, given the proof statuses"""
     js_plan, sp_plan, out_plan = plan
     if sp_ok is None:
@@ -171,7 +185,7 @@ def _tx_error(tx, plan, status, sp_ok=None, bind_ok=None):
         if not tx.js_sig_ok:
             return "JoinSplitSignature"
         for i, (d, (how, v)) in enumerate(zip(tx.joinsplits, js_plan)):
-            ok = v if how == "caller" else status[v] == OK
+            ok = v if how == "caller" else (pghr_status[v] if how == "pghr" else status[v]) == OK
             if not ok:
                 return ("InvalidJoinSplit", i)
             if d.tree_error:
@@ -210,7 +224,7 @@ def _chunked(verify, cap):
     return run
 
 
-def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None):
+def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None, verify_pghr=None):
     """Check the shielded proofs of a block (or an import window: a flat list of Tx in chain
     order). Returns None if every transaction passes, else (tx_index, error) with the error the
     reference reports (accept_chain.rs:79-80: the lowest failing index wins).
@@ -219,8 +233,10 @@ def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None)
     batch for the whole block, exact per-proof statuses via bisection). A window larger than
     the context's max_batch (or a `verify.max_batch` attribute) is split into consecutive
     batches. Transactions that carry their sighash get their RedJubjub signatures verified on
-    the GPU too (verify_sigs / sapling_bvk default to ctx.redjubjub_verify / ctx.sapling_bvk)."""
-    items, plans = _queue(txs)
+    the GPU too (verify_sigs / sapling_bvk default to ctx.redjubjub_verify / ctx.sapling_bvk).
+    PHGR JoinSplit proofs go through verify_pghr(proofs, inputs) -> statuses, default
+    ctx.pghr13_verify (ONE zg_pghr13_verify call for the window)."""
+    items, pghr, plans = _queue(txs)
     if verify is None:
         def verify(proofs, kinds, inputs, n_inputs):
             return ctx.verify_batch(proofs, kinds, inputs, n_inputs)[0]
@@ -235,9 +251,16 @@ def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None)
         inputs = zg.pack_inputs([inp for _, _, inp in items])
         n_inputs = bytes(len(inp) for _, _, inp in items)
         status = list(verify(proofs, kinds, inputs, n_inputs))
+    pghr_status = []
+    if pghr:
+        if verify_pghr is None:
+            if ctx is None:
+                raise zg.ZgError(-1, "PHGR JoinSplits in the window but no PGHR13 backend (pass ctx= or verify_pghr=)")
+            verify_pghr = ctx.pghr13_verify
+        pghr_status = list(verify_pghr([p for p, _ in pghr], [inp for _, inp in pghr]))
     sp_ok, bind_ok = _sig_verdicts(txs, ctx, verify_sigs, sapling_bvk)
     for idx, (tx, plan) in enumerate(zip(txs, plans)):
-        err = _tx_error(tx, plan, status, sp_ok[idx], bind_ok[idx])
+        err = _tx_error(tx, plan, status, sp_ok[idx], bind_ok[idx], pghr_status)
         if err is not None:
             return idx, err
     return None

@@ -47,11 +47,11 @@ int merkle_tree_roots(MerkleDev* m, hipStream_t st, int kind, int height, const 
                       void** arena, size_t* arena_cap, std::string* err);
 // zg_pghr13.hip
 struct BnDev;
+struct BnKey;
 BnDev* bn_dev_new();
 void bn_dev_free(BnDev* d);
-int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, std::string* err);
-bool bn_vk_loaded(BnDev* d);
-int bn_pghr13_verify(BnDev* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
+int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, const BnKey** out, std::string* err);
+int bn_pghr13_verify(const BnKey* k, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
                      const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
                      std::string* err);
 int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt, std::string* err);
@@ -149,6 +149,9 @@ struct zg_ctx {
   // [6] K4 bucket entries of the last batch (points with a non-zero digit, summed over windows)
   uint64_t stats[ZG_NSTATS] = {};
   uint64_t calls = 0;
+  int debug_each = 0;         // ZG_DEBUG_EACH=1: every batch's statuses re-checked per proof
+  uint8_t* d_dbg = nullptr;   // the per-proof statuses of that re-check
+  const zg::BnKey* bn_key = nullptr;  // this slot's PGHR13 key (an immutable entry of the device cache)
   void* tree_arena = nullptr;  // zg_tree_roots scratch (grow-only, zg_merkle.hip)
   size_t tree_arena_cap = 0;
 };
@@ -164,8 +167,6 @@ static int fail(zg_ctx* c, int code, const std::string& msg) {
   } while (0)
 
 static unsigned nblocks(size_t n) { return (unsigned)((n + ZG_BLOCK - 1) / ZG_BLOCK); }
-
-extern "C" const char* zg_version(void) { return "zebra_amd zg 0.2 gfx950"; }
 
 extern "C" const char* zg_last_error(zg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
@@ -258,6 +259,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
+  if (const char* e = getenv("ZG_DEBUG_EACH")) ctx->debug_each = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
     if (e == hipSuccess) e = r;
@@ -292,6 +294,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_pairf, (size_t)ZG_NODE_CHUNK * ZG_NODE_PAIRS));
   A(dalloc(&ctx->d_ok, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_out, ZG_NODE_CHUNK));
+  if (ctx->debug_each) A(dalloc(&ctx->d_dbg, cap));
   for (int i = 0; i < ZG_NEV; i++) A(hipEventCreate(&ctx->ev[i]));
   // surface a broken device / stream now rather than inside a later batch
   A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
@@ -320,7 +323,8 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
-                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena};
+                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
+                  ctx->d_dbg};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -1075,6 +1079,23 @@ static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool 
     }
   }
   for (size_t i = 0; i < ctx->n; i++) status[i] = st[i] == ST_PENDING ? ST_OK : st[i];
+  if (ctx->debug_each && ctx->n) {
+    // debug cross-check: bellman's per-proof verify_proof (k_verify_single, one pairing check per
+    // proof, no batch scalars) on the batch's own device inputs must give the same statuses
+    const size_t n = ctx->n;
+    hipLaunchKernelGGL(k_verify_single, dim3(nblocks(n)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_vk, (int)n,
+                       ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->cur_ninputs, ctx->d_dbg, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(st.data(), ctx->d_dbg, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < n; i++)
+      if (st[i] != status[i]) {
+        set_state(ctx, 0);
+        return fail(ctx, ZG_E_DEBUG, "ZG_DEBUG_EACH: proof " + std::to_string(i) + ": batch status " +
+                                         std::to_string(status[i]) + ", per-proof verify_proof status " +
+                                         std::to_string(st[i]));
+      }
+  }
   set_state(ctx, 0);
   return ZG_OK;
 }
@@ -1263,6 +1284,16 @@ extern "C" int zg_prep_joinsplit(const uint8_t anchor[32], const uint8_t random_
   if (!anchor || !random_seed || !nullifiers || !macs || !commitments || !pubkey || !inputs) return ZG_E_INVAL;
   prep_joinsplit(anchor, random_seed, nullifiers, nullifiers + 32, macs, macs + 32, commitments, commitments + 32,
                  vpub_old, vpub_new, pubkey, inputs);
+  return ZG_OK;
+}
+
+extern "C" int zg_prep_joinsplit_bn(const uint8_t anchor[32], const uint8_t random_seed[32],
+                                    const uint8_t nullifiers[64], const uint8_t macs[64],
+                                    const uint8_t commitments[64], uint64_t vpub_old, uint64_t vpub_new,
+                                    const uint8_t pubkey[32], uint8_t inputs[9 * 32]) {
+  if (!anchor || !random_seed || !nullifiers || !macs || !commitments || !pubkey || !inputs) return ZG_E_INVAL;
+  prep_joinsplit_bits(anchor, random_seed, nullifiers, nullifiers + 32, macs, macs + 32, commitments,
+                      commitments + 32, vpub_old, vpub_new, pubkey, 253, inputs);
   return ZG_OK;
 }
 
@@ -1470,11 +1501,20 @@ static zg::BnDev* bn_dev(zg_ctx* ctx) {
   return d->bn;
 }
 
+// a key is parsed, prepared into fresh buffers and published in the device cache, then this
+// context points at it (other contexts keep theirs); a failed load leaves the context's key as it was
+static int pghr13_load_locked(zg_ctx* ctx, const char* json, size_t len) {
+  HIPCHK(hipSetDevice(ctx->device));
+  const zg::BnKey* k = nullptr;
+  const int rc = bn_load_vk_json(bn_dev(ctx), ctx->stream, json, len, &k, &ctx->err);
+  if (rc == ZG_OK) ctx->bn_key = k;
+  return rc;
+}
+
 extern "C" int zg_pghr13_vk_load_json(zg_ctx* ctx, const char* json, size_t len) {
   if (!ctx || !json) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
-  return bn_load_vk_json(bn_dev(ctx), ctx->stream, json, len, &ctx->err);
+  return pghr13_load_locked(ctx, json, len);
 }
 
 extern "C" int zg_pghr13_vk_load_builtin(zg_ctx* ctx) {
@@ -1487,12 +1527,11 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
   if (n_inputs)
     for (size_t i = 0; i < n; i++)
       if (n_inputs[i] > 9) return fail(ctx, ZG_E_INVAL, "at most 9 PGHR13 inputs per proof");
-  zg::BnDev* d = bn_dev(ctx);
-  if (!bn_vk_loaded(d)) {
-    int rc = zg_pghr13_vk_load_builtin(ctx);
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->bn_key) {  // first use: the builtin key (res/sprout-verifying-key.json)
+    int rc = pghr13_load_locked(ctx, ZG_PGHR13_VK_JSON, strlen(ZG_PGHR13_VK_JSON));
     if (rc) return rc;
   }
-  std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   if (!n) return ZG_OK;
   // the equality weights rho_2..rho_5 (16 bytes each): seeded contexts (tests) derive them,
@@ -1512,7 +1551,8 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
   } else if (!os_random(rho.data(), rho.size())) {
     return fail(ctx, ZG_E_INVAL, "getrandom failed");
   }
-  return bn_pghr13_verify(d, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status, kernel_ms, &ctx->err);
+  return bn_pghr13_verify(ctx->bn_key, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status, kernel_ms,
+                          &ctx->err);
 }
 
 extern "C" int zg_bn254_pairing(zg_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt) {

@@ -331,20 +331,34 @@ __global__ void __launch_bounds__(64) k_bn_gt(int n, Bq12* w, uint32_t* gt) {
 }
 
 // ------------------------------------------------------------------ host side
-struct BnDev {
-  std::mutex mu;
+// One prepared PGHR13 key: the key, its line table and comb tables. Built into fresh buffers
+// and published in the device's cache only once complete and valid; never modified or freed
+// while the device lives, so a context verifying with it needs no lock (a key loaded on one
+// context does not change the key of any other context).
+struct BnKey {
+  std::vector<uint32_t> raw;  // the parsed key words (the cache key)
   BnVK* vk = nullptr;
   BLine* lines = nullptr;
   uint32_t* comb = nullptr;
-  int err = 0;  // the loaded key failed AffineG*::new
 };
+
+struct BnDev {
+  std::mutex mu;                // the cache
+  std::vector<BnKey*> keys;     // every distinct key loaded on this device
+};
+
+static void bn_key_free(BnKey* k) {
+  if (!k) return;
+  if (k->vk) hipFree(k->vk);
+  if (k->lines) hipFree(k->lines);
+  if (k->comb) hipFree(k->comb);
+  delete k;
+}
 
 BnDev* bn_dev_new() { return new BnDev(); }
 void bn_dev_free(BnDev* d) {
   if (!d) return;
-  if (d->vk) hipFree(d->vk);
-  if (d->lines) hipFree(d->lines);
-  if (d->comb) hipFree(d->comb);
+  for (BnKey* k : d->keys) bn_key_free(k);
   delete d;
 }
 
@@ -402,8 +416,7 @@ static bool hex_fq(const std::string& h, uint32_t* w) {
   return false;
 }
 
-int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, std::string* err) {
-  std::lock_guard<std::mutex> g(d->mu);
+int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, const BnKey** out, std::string* err) {
   const std::string js(json, len);
   std::vector<uint32_t> raw;
   auto put = [&](const std::string& h) {
@@ -442,46 +455,53 @@ int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, std:
       return ZG_E_VK;
     }
   const int ic_len = (int)ic.size() / 2;
-  if (!d->vk) {
-    BCHK(hipMalloc(&d->vk, sizeof(BnVK)));
-    BCHK(hipMalloc(&d->lines, sizeof(BLine) * ZG_BN_FIXED_Q * ZG_BN_NLINES));
-    BCHK(hipMalloc(&d->comb, (size_t)ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D * 64));
-  }
-  uint32_t* draw;
-  BCHK(hipMalloc(&draw, raw.size() * 4));
-  hipError_t e = hipMemcpyAsync(draw, raw.data(), raw.size() * 4, hipMemcpyHostToDevice, st);
+  std::lock_guard<std::mutex> g(d->mu);  // one build per distinct key, never a half-built entry visible
+  for (BnKey* k : d->keys)
+    if (k->raw == raw) {
+      *out = k;
+      return ZG_OK;
+    }
+  BnKey* k = new BnKey();
+  k->raw = raw;
+  uint32_t* draw = nullptr;
+  int verr = 0;
+  hipError_t e = hipMalloc(&k->vk, sizeof(BnVK));
+  if (e == hipSuccess) e = hipMalloc(&k->lines, sizeof(BLine) * ZG_BN_FIXED_Q * ZG_BN_NLINES);
+  if (e == hipSuccess) e = hipMalloc(&k->comb, (size_t)ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D * 64);
+  if (e == hipSuccess) e = hipMalloc(&draw, raw.size() * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(draw, raw.data(), raw.size() * 4, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_bn_vk, dim3(1), dim3(64), 0, st, draw, ic_len, d->vk);
+    hipLaunchKernelGGL(k_bn_vk, dim3(1), dim3(64), 0, st, draw, ic_len, k->vk);
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_bn_lines, dim3(1), dim3(64), 0, st, d->vk, d->lines);
+    hipLaunchKernelGGL(k_bn_lines, dim3(1), dim3(64), 0, st, k->vk, k->lines);
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_bn_comb, dim3(bn_blocks(ZG_BN_COMB_BASES * ZG_BN_COMB_W * ZG_BN_COMB_D)), dim3(64), 0, st,
-                       d->vk, d->comb);
+                       k->vk, k->comb);
     e = hipGetLastError();
   }
-  int verr = 0;
-  if (e == hipSuccess) e = hipMemcpyAsync(&verr, &d->vk->err, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(&verr, &k->vk->err, sizeof(int), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  hipFree(draw);
+  if (draw) hipFree(draw);
   if (e != hipSuccess) {
+    bn_key_free(k);
     *err = std::string("PGHR13 key upload: ") + hipGetErrorString(e);
     return ZG_E_HIP;
   }
-  d->err = verr;
   if (verr) {
+    bn_key_free(k);
     *err = "PGHR13 key: a point is not on its curve or not of order r (AffineG*::new)";
     return ZG_E_VK;
   }
+  d->keys.push_back(k);
+  *out = k;
   return ZG_OK;
 }
 
-bool bn_vk_loaded(BnDev* d) { return d->vk && !d->err; }
-
-int bn_pghr13_verify(BnDev* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
+int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
                      const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
                      std::string* err) {
   if (!n) return ZG_OK;

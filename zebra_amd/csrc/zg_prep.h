@@ -207,11 +207,14 @@ inline void prep_hsig(const uint8_t* seed, const uint8_t* nf0, const uint8_t* nf
 }
 
 // sprout.rs:42-58,86-153: the 2176-bit string (bytes MSB-first) of anchor, hSig, nf0, mac0,
-// nf1, mac1, cm0, cm1, vpub_old (u64 LE), vpub_new (u64 LE), cut into 254-bit chunks, each
-// read with its first bit as the least significant (into_bls_frs) -> 9 Fr
-inline void prep_joinsplit(const uint8_t* anchor, const uint8_t* seed, const uint8_t* nf0, const uint8_t* nf1,
-                           const uint8_t* mac0, const uint8_t* mac1, const uint8_t* cm0, const uint8_t* cm1,
-                           uint64_t vpub_old, uint64_t vpub_new, const uint8_t* pubkey, uint8_t* out) {
+// nf1, mac1, cm0, cm1, vpub_old (u64 LE), vpub_new (u64 LE), cut into `chunk`-bit pieces, each
+// read with its first bit as the least significant -> 9 field elements (32 B LE). chunk = 254
+// (bls::Fr::CAPACITY, into_bls_frs: the Groth16 branch) or 253 (into_bn_frs: the PHGR branch,
+// sprout.rs:119-133); either way a piece is < 2^254 and below the field's modulus.
+inline void prep_joinsplit_bits(const uint8_t* anchor, const uint8_t* seed, const uint8_t* nf0, const uint8_t* nf1,
+                                const uint8_t* mac0, const uint8_t* mac1, const uint8_t* cm0, const uint8_t* cm1,
+                                uint64_t vpub_old, uint64_t vpub_new, const uint8_t* pubkey, int chunk,
+                                uint8_t* out) {
   uint8_t hsig[32], vo[8], vn[8];
   prep_hsig(seed, nf0, nf1, pubkey, hsig);
   for (int k = 0; k < 8; k++) {
@@ -226,9 +229,15 @@ inline void prep_joinsplit(const uint8_t* anchor, const uint8_t* seed, const uin
     for (int k = 0; k < lens[p]; k++)
       for (int j = 7; j >= 0; j--, bit++)
         if ((parts[p][k] >> j) & 1u) {
-          const int chunk = bit / 254, pos = bit % 254;  // < 2^254 < r: already reduced
-          out[32 * chunk + pos / 8] |= (uint8_t)(1u << (pos % 8));
+          const int c = bit / chunk, pos = bit % chunk;
+          out[32 * c + pos / 8] |= (uint8_t)(1u << (pos % 8));
         }
+}
+
+inline void prep_joinsplit(const uint8_t* anchor, const uint8_t* seed, const uint8_t* nf0, const uint8_t* nf1,
+                           const uint8_t* mac0, const uint8_t* mac1, const uint8_t* cm0, const uint8_t* cm1,
+                           uint64_t vpub_old, uint64_t vpub_new, const uint8_t* pubkey, uint8_t* out) {
+  prep_joinsplit_bits(anchor, seed, nf0, nf1, mac0, mac1, cm0, cm1, vpub_old, vpub_new, pubkey, 254, out);
 }
 
 }  // namespace zg

@@ -16,19 +16,19 @@ def shard_range(n, world, rank):
 _xbufs = {}
 
 
-def _exchange_buffers(world, device):
-    """per (device, world): the staging buffers of combine_partials, allocated once (pinned host
-    memory and a high-priority stream on a GPU, so the 576-B copies are DMA enqueues that do not
-    wait behind in-flight batches)"""
+def _exchange_buffers(world, device, k):
+    """per (device, world, k): the staging buffers of combine_partials, allocated once (pinned
+    host memory and a high-priority stream on a GPU, so the k x 576-B copies are DMA enqueues
+    that do not wait behind in-flight batches)"""
     import torch
-    key = (str(device), world)
+    key = (str(device), world, k)
     if key not in _xbufs:
         gpu = torch.device(device).type == "cuda"
         stream = torch.cuda.Stream(device=device, priority=-1) if gpu else None
-        _xbufs[key] = (torch.empty(GT_BYTES, dtype=torch.uint8, pin_memory=gpu),
-                       torch.empty(GT_BYTES, dtype=torch.uint8, device=device),
-                       torch.empty(world * GT_BYTES, dtype=torch.uint8, device=device),
-                       torch.empty(world * GT_BYTES, dtype=torch.uint8, pin_memory=gpu), stream)
+        _xbufs[key] = (torch.empty(k * GT_BYTES, dtype=torch.uint8, pin_memory=gpu),
+                       torch.empty(k * GT_BYTES, dtype=torch.uint8, device=device),
+                       torch.empty(world * k * GT_BYTES, dtype=torch.uint8, device=device),
+                       torch.empty(world * k * GT_BYTES, dtype=torch.uint8, pin_memory=gpu), stream)
     return _xbufs[key]
 
 
@@ -39,20 +39,28 @@ def combine_partials(partial, check, world, rank, device):
     without a second collective (ncclAllGather when every rank needs the result).
     Keeping the exchange to one collective matters with batches in flight: every extra device
     op queues behind the other batches' kernels. Calls must not overlap (the staging buffers are
-    reused; run_pipelined* issue them from one thread, in batch order)."""
+    reused; run_pipelined* issue them from one thread, in batch order).
+
+    `partial` is one 576-B partial, or a list of k of them when a rank verifies k shards of the
+    batch (every rank must pass the same k): the gather then moves world x k partials in the
+    same single collective, ordered rank-major (rank 0's k shards first)."""
     import contextlib
     import numpy as np
     import torch
     import torch.distributed as dist
-    assert len(partial) == GT_BYTES
-    host, mine, flat, back, stream = _exchange_buffers(world, device)
+    parts = [partial] if isinstance(partial, (bytes, bytearray)) else list(partial)
+    k = len(parts)
+    assert k >= 1 and all(len(p) == GT_BYTES for p in parts)
+    host, mine, flat, back, stream = _exchange_buffers(world, device, k)
     with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
-        host.numpy()[:] = np.frombuffer(partial, dtype=np.uint8)
+        host.numpy()[:] = np.frombuffer(b"".join(parts), dtype=np.uint8)
         mine.copy_(host, non_blocking=True)
         dist.all_gather_into_tensor(flat, mine)
         back.copy_(flat)
+    if stream is not None:
+        stream.synchronize()
     allb = back.numpy().tobytes()
-    return check([allb[GT_BYTES * r:GT_BYTES * (r + 1)] for r in range(world)])
+    return check([allb[GT_BYTES * j:GT_BYTES * (j + 1)] for j in range(world * k)])
 
 
 def run_pipelined(ctxs, k, launch, complete):

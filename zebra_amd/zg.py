@@ -13,6 +13,7 @@ GEN_SPEND_AUTH, GEN_BINDING = 0, 1   # include/zg.h ZG_GEN_*
 TREE_SPROUT, TREE_SAPLING = 0, 1     # include/zg.h ZG_TREE_*
 SPROUT_HEIGHT, SAPLING_HEIGHT = 29, 32   # storage/src/tree_state.rs H29 / H32
 E_TREE_FULL = -7
+E_DEBUG = -8     # ZG_DEBUG_EACH=1: batch statuses differ from the per-proof re-check
 KIND_NINPUTS = {KIND_SPEND: 7, KIND_OUTPUT: 5, KIND_SPROUT: 9}
 STATUS_OK, STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "DECODE_INVALID", 2: "MALFORMED_VK", 3: "VERIFY_FAILED", 4: "INPUT_NONCANONICAL"}
@@ -85,7 +86,9 @@ def lib():
         L.zg_prep_spend.argtypes = [u8p, u8p, u8p, u8p, u8p]
         L.zg_prep_output.argtypes = [u8p, u8p, u8p, u8p]
         L.zg_prep_joinsplit.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
+        L.zg_prep_joinsplit_bn.argtypes = [u8p, u8p, u8p, u8p, u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, u8p]
         L.zg_hsig.argtypes = [u8p, u8p, u8p, u8p, u8p]
+        L.zg_debug_field_mul.argtypes = [i, i, sz, u8p, u8p, u8p]
         _lib = L
     return _lib
 
@@ -133,12 +136,36 @@ def prep_joinsplit(anchor, random_seed, nullifiers, macs, commitments, vpub_old,
                                          vpub_old, vpub_new, bytes(pubkey), out), out, 9)
 
 
+def prep_joinsplit_bn(anchor, random_seed, nullifiers, macs, commitments, vpub_old, vpub_new, pubkey):
+    """the PHGR branch's input (sprout.rs:34-67, Input::into_bn_frs: 253-bit chunks) -> 9 x
+    32-byte LE BN254 Fr"""
+    out = ctypes.create_string_buffer(9 * 32)
+    return _prep(lib().zg_prep_joinsplit_bn(bytes(anchor), bytes(random_seed), b"".join(map(bytes, nullifiers)),
+                                            b"".join(map(bytes, macs)), b"".join(map(bytes, commitments)),
+                                            vpub_old, vpub_new, bytes(pubkey), out), out, 9)
+
+
 def hsig(random_seed, nf0, nf1, pubkey):
     out = ctypes.create_string_buffer(32)
     rc = lib().zg_hsig(bytes(random_seed), bytes(nf0), bytes(nf1), bytes(pubkey), out)
     if rc:
         raise ZgError(rc, "bad argument")
     return out.raw
+
+
+FIELD_BYTES = {0: 48, 1: 48, 2: 96, 3: 32, 4: 32}   # zg_debug_field_mul operand sizes
+
+
+def debug_field_mul(field, a, b, device=0):
+    """zg_debug_field_mul: the device's Montgomery product for each pair (lists of LE bytes)"""
+    w = FIELD_BYTES[field]
+    n = len(a)
+    assert len(b) == n and all(len(x) == w for x in a) and all(len(x) == w for x in b)
+    out = ctypes.create_string_buffer(max(1, w * n))
+    rc = lib().zg_debug_field_mul(device, field, n, b"".join(a), b"".join(b), out)
+    if rc:
+        raise ZgError(rc, "zg_debug_field_mul")
+    return [out.raw[w * i:w * i + w] for i in range(n)]
 
 
 def pack_inputs(rows):
@@ -315,8 +342,12 @@ class Context:
 
     # ---- PGHR13 Sprout proofs on BN254 (include/zg.h zg_pghr13_* / zg_bn254_pairing)
     def pghr13_vk_load_json(self, text):
+        """this context's PGHR13 key (other contexts keep theirs; a failed load keeps the old one)"""
         b = text.encode() if isinstance(text, str) else bytes(text)
         self._chk(lib().zg_pghr13_vk_load_json(self._p, b, len(b)))
+
+    def pghr13_vk_load_builtin(self):
+        self._chk(lib().zg_pghr13_vk_load_builtin(self._p))
 
     def pghr13_verify(self, proofs, inputs, n_inputs=None, with_time=False):
         """proofs: 296-byte PHGR proofs; inputs: per proof a list of <= 9 32-byte LE BN254 Fr
