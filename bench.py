@@ -106,7 +106,10 @@ def cpu_threads(requested=0):
 
 def cpu_baseline(proofs, kinds, inputs, seconds, threads):
     """the oracle's C++ restatement of bellman's per-proof verify, on host cores, on a bounded
-    sample of the same workload."""
+    sample of the same workload. `threads` is this job's CPU share on the box (OMP_NUM_THREADS;
+    the pool's rules keep a one-GPU job's worker pools to that share), so the all-core figure of
+    SURVEY.md 8(d) is reported beside it as a projection: the measured per-thread rate x every
+    usable CPU, with the measured 1 -> `threads` scaling efficiency that justifies it."""
     from tests import cpulib
     L = cpulib.load()
     n = len(kinds)
@@ -119,13 +122,25 @@ def cpu_baseline(proofs, kinds, inputs, seconds, threads):
     sts, _ = cpulib.verify(L, proofs[:192 * m], kinds[:m], inputs[:288 * m], threads=threads)
     dt = time.perf_counter() - t
     assert all(s == 0 for s in sts), "cpu baseline rejected a valid proof"
+    # one thread on a short sample: the scaling efficiency of the threaded figure
+    m1 = max(8, int(m / threads / 6))
+    t = time.perf_counter()
+    cpulib.verify(L, proofs[:192 * m1], kinds[:m1], inputs[:288 * m1], threads=1)
+    rate1 = m1 / (time.perf_counter() - t)
     h = host_cpu()
-    return {"value": m / dt, "unit": "proofs/s", "cores": threads, "kind": "port",
+    value = m / dt
+    return {"value": value, "unit": "proofs/s", "cores": threads, "kind": "port",
             "nproc": h["nproc"], "usable_cpus": h["usable"], "cpu_model": h["cpu_model"],
             "ms_per_proof_per_core": 1e3 * dt * threads / m,
+            "one_thread_proofs_per_s": rate1, "scaling_efficiency": value / (threads * rate1),
+            "projected_all_usable_cpus": {
+                "value": value / threads * h["usable"], "cpus": h["usable"],
+                "note": "measured per-thread rate x usable CPUs (linear scaling, the one-proof-per-task "
+                        "fan-out has no shared state); not measured: the box grants a one-GPU job %d of "
+                        "its CPUs (OMP_NUM_THREADS) and its worker pools are kept to that share" % threads},
             "sample": "first %d proofs of the same re-randomized 65,536-proof workload, bellman-restatement "
                       "per-proof verify_proof (oracle/cpu/bellman_cpu.cpp), one proof per std::thread task on "
-                      "%d threads, %.1f s" % (m, threads, dt)}
+                      "%d threads, %.1f s; one thread: %d proofs" % (m, threads, dt, m1)}
 
 
 def h2d_copy_ms(proofs, kinds, inputs, dev, reps=5):
@@ -466,7 +481,7 @@ def main():
         for name, kind, h in (("sapling_h32", _zg.TREE_SAPLING, 32), ("sprout_h29", _zg.TREE_SPROUT, 29)):
             trees[name] = bench_tree.run(ctx, kind, h, 65536, 64, 10)
             if not args.no_cpu:
-                trees[name]["cpu_baseline"] = bench_tree.cpu_window(kind, h, 64, 4.0)
+                trees[name]["cpu_baseline"] = bench_tree.cpu_window(kind, h, 64, 4.0, cpu_threads(args.cpu_threads))
                 trees[name]["gpu_over_cpu"] = trees[name]["leaves_per_s"] / trees[name]["cpu_baseline"]["leaves_per_s"]
         out["note_commitment_trees"] = trees
         # PGHR13 Sprout proofs on BN254 (tools/bench_pghr13.py), not the headline
@@ -475,12 +490,13 @@ def main():
         pg["workload"] = ("65,536 PHGR JoinSplit proofs cycling through the 9 valid reference / block-522 "
                           "statements; host buffers (zg_pghr13_verify)")
         if not args.no_cpu:
-            pg["cpu_baseline"] = bench_pghr13.cpu_baseline(4.0)
+            pg["cpu_baseline"] = bench_pghr13.cpu_baseline(4.0, cpu_threads(args.cpu_threads))
             pg["gpu_over_cpu"] = pg["proofs_per_s"] / pg["cpu_baseline"]["proofs_per_s"]
         out["pghr13_sprout_proofs"] = pg
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(proofs, kinds, inputs, args.cpu_seconds, cpu_threads(args.cpu_threads))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu_all_usable_projected"] = value / out["cpu_baseline"]["projected_all_usable_cpus"]["value"]
     st = {}
     for c in ctxs:
         for k, v in c.stats().items():

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-3 GPU pass: gpu tests, smoke, the driver's bench command (timed), optionally rocprofv3
+# kernel stats of the bench. Usage (repo root on the box): bash tools/gpu_r03.sh TAG [tests|bench|prof]...
+set -o pipefail
+TAG=${1:-r03}
+shift
+STEPS=${*:-tests bench}
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+nproc > $O/host.txt; grep -m1 "model name" /proc/cpuinfo >> $O/host.txt; echo "OMP=$OMP_NUM_THREADS" >> $O/host.txt
+for s in $STEPS; do
+  case $s in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -60 $O/gpu_tests.log; exit 1; }
+    tail -3 $O/gpu_tests.log
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+    tail -1 $O/smoke.log ;;
+  bench)
+    t0=$(date +%s.%N)
+    timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+    t1=$(date +%s.%N)
+    echo "driver bench wall s: $(python3 -c "print($t1-$t0)")" | tee $O/bench_wall.txt
+    python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['phase_ms'])" ;;
+  quick)
+    timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_quick.json 2> $O/bench_quick.err || { echo "bench quick failed"; tail -30 $O/bench_quick.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_quick.json')); print('64k', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
+    timeout -k 10 200 python -u bench.py --no-cpu --no-configs --proofs 8192 > $O/bench_8192.json 2> $O/bench_8192.err || { echo "bench 8192 failed"; tail -30 $O/bench_8192.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_8192.json')); print('8k', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')" ;;
+  prof)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof_bench_iso.json 2> $O/prof_bench_iso.err || { echo "rocprof iso failed"; tail -30 $O/prof_bench_iso.err; exit 1; }
+    cd $R && for k in prof prof_iso; do python3 tools/rocpd_stats.py $O/$k/run_results.db $O/kernel_stats_${k#prof}.csv; done ;;
+  esac
+done
