@@ -41,9 +41,15 @@ W_TREE = 54                                  # tree-product Fq12 multiply
 W_TOTAL = 13622
 assert W_DECODE + W_K4 + W_LINES + W_FCHAIN + W_TREE == W_TOTAL
 # K4 bucket phase, algorithmic HBM bytes: per entry the 4-byte bucket entry and the 100-byte
-# affine C_i it names (G1A), plus the partial bucket sums written once (Jacobian, 144 B)
+# affine C_i it names (G1A), plus the bucket offsets read and the (T, U) segment sums written
+# (Jacobian, 144 B each) -- zg_msm.h msm_shape: c = 11 from 32k padded proofs, 10 from 8k, 9 below
 K4_ENTRY_BYTES = 4 + 100
-K4_BSUM_BYTES = 3 * 6 * 1024 * 4 * 144
+
+
+def k4_fixed_bytes(npad):
+    c, w, nb, parts = (11, 6, 1024, 4) if npad >= 32768 else (10, 7, 512, 2) if npad >= 8192 else (9, 8, 256, 1)
+    ncount = 3 * w * nb
+    return ncount * 4 + (ncount // (64 // parts)) * 2 * 144
 NOMINAL_LANES = 256 * 4 * 16                        # MI355X: CUs x SIMDs x lanes per clock
 MACS_PER_FQMUL = 288                                # 2 * 12^2 32x32->64 MACs (product + CIOS reduction)
 
@@ -423,7 +429,8 @@ def main():
         traffic, k4_traffic = pt.get(rk), pt.get("k_msm_bucket")
     k4 = None
     if k4_entries is not None and iso_avg[8] > 0:
-        k4_bytes = k4_entries * K4_ENTRY_BYTES + K4_BSUM_BYTES
+        npad = 1 << max(1, (shard - 1).bit_length())
+        k4_bytes = k4_entries * K4_ENTRY_BYTES + k4_fixed_bytes(npad)
         k4 = {"kernel": "k_msm_bucket", "bound": "hbm", "entries": k4_entries, "algorithmic_bytes": k4_bytes,
               "ms": iso_avg[8], "achieved_gbs": k4_bytes / (iso_avg[8] * 1e-3) / 1e9, "peak_gbs": 8000.0,
               "frac": k4_bytes / (iso_avg[8] * 1e-3) / 8e12, "traffic": k4_traffic,

@@ -6,6 +6,7 @@
 #include "../../zebra_amd/csrc/zg_groth16.h"
 #include "../../zebra_amd/csrc/zg_bingcd.h"
 #include "../../zebra_amd/csrc/zg_bn254.h"
+#include "../../zebra_amd/csrc/zg_lines.h"
 
 using namespace zg;
 
@@ -13,6 +14,38 @@ static Fq ld_fq(const uint8_t* b) { return fq_to_mont(fq_limbs_from_be(b)); }
 static void st_fq(const Fq& a, uint8_t* b) { fq_limbs_to_be(fq_from_mont(a), b); }
 
 extern "C" {
+
+// the R-chain of zg_lines.h (k_batch_lines_lane) for one proof: B (x.c0 x.c1 y.c0 y.c1) and
+// P = r A (x y), 48-byte BE each, canonical -> 68 x 3 scaled line coefficients (Fq2 as c0 || c1,
+// BE) and, for comparison, the same from g2_prepare + the ell scaling (zg_pairing.h)
+void zgt_lines_lane(const uint8_t* q, const uint8_t* p, uint8_t* out_lane, uint8_t* out_ref) {
+  G2A B = {{ld_fq(q), ld_fq(q + 48)}, {ld_fq(q + 96), ld_fq(q + 144)}, false};
+  G1A P = {ld_fq(p), ld_fq(p + 48), false};
+  auto st2 = [](const Fq2& v, uint8_t* o) {
+    st_fq(v.c0, o);
+    st_fq(v.c1, o + 48);
+  };
+  G2J r = {B.x, B.y, f2_one()};
+  Fq2 l[3];
+  int n = 0;
+  for (int i = ZG_XH_TOP; i >= -1; i--) {
+    ls_double(r, &P, l, true);
+    for (int j = 0; j < 3; j++) st2(l[j], out_lane + (n * 3 + j) * 96);
+    n++;
+    if (i >= 0 && ((ZG_XH >> i) & 1ull)) {
+      ls_add(r, &B, &P, l, true);
+      for (int j = 0; j < 3; j++) st2(l[j], out_lane + (n * 3 + j) * 96);
+      n++;
+    }
+  }
+  static Line ref[ZG_NCOEFF];
+  g2_prepare(B, ref);
+  for (int k = 0; k < ZG_NCOEFF; k++) {
+    st2(ref[k].c2, out_ref + (k * 3 + 0) * 96);
+    st2(f2_mul_fq(ref[k].c1, P.x), out_ref + (k * 3 + 1) * 96);
+    st2(f2_mul_fq(ref[k].c0, P.y), out_ref + (k * 3 + 2) * 96);
+  }
+}
 
 // the products of zg_debug_field_mul (zebra_amd/csrc/zg_debug.hip) on the host: same field ids
 void zgt_field_mul(int field, const uint32_t* a, const uint32_t* b, uint32_t* r) {

@@ -206,3 +206,75 @@ def test_config3_eight_shards_one_gpu(workload3, cpu):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_config3_gt_split_invariance(workload3, cpu):
+    """size-independent GT parity at the full 65,536: with the same explicit batch scalars, the
+    accumulated GT of the whole batch (four proofs per f-chain lane, K4 at c = 11) equals the
+    product of the GTs of its 8 x 8,192 shards (c = 10) and of its 16 x 4,096 shards (two proofs
+    per lane, c = 9); and for 64 random indices of the same workload the device GT equals the
+    oracle's prod LHS_i^{r_i} (C++ restatement of bellman's per-proof left-hand sides)"""
+    from oracle import bls12_381 as B, groth16 as G
+    from tests import cpulib
+    from zebra_amd import Context
+    proofs, kinds, inputs, _ = workload3
+    n = 65536
+    r = random.Random(11).randbytes(16 * n)
+    big = Context(device=0, max_batch=n)
+    try:
+        sts, gt_full = big.verify_batch(proofs, kinds, inputs, r=r, want_gt=True)
+        assert sts == [0] * n and big.stats()["quad_fchain_launches"] >= 1
+    finally:
+        big.close()
+    for shard in (8192, 4096):
+        c = Context(device=0, max_batch=shard)
+        try:
+            acc = B.F12_ONE
+            for lo in range(0, n, shard):
+                hi = lo + shard
+                s, g = c.verify_batch(proofs[192 * lo:192 * hi], kinds[lo:hi], inputs[288 * lo:288 * hi],
+                                      r=r[16 * lo:16 * hi], want_gt=True)
+                assert s == [0] * shard
+                acc = B.f12_mul(acc, B.f12_from_bytes(g))
+        finally:
+            c.close()
+        assert B.f12_to_bytes(acc) == gt_full, shard
+    idx = sorted(random.Random(12).sample(range(n), 64))
+    sp = b"".join(proofs[192 * i:192 * i + 192] for i in idx)
+    sk = bytes(kinds[i] for i in idx)
+    sx = b"".join(inputs[288 * i:288 * i + 288] for i in idx)
+    sr = b"".join(r[16 * i:16 * i + 16] for i in idx)
+    c = Context(device=0, max_batch=64)
+    try:
+        s, g = c.verify_batch(sp, sk, sx, r=sr, want_gt=True)
+    finally:
+        c.close()
+    osts, lhs = cpulib.verify(cpu, sp, sk, sx, threads=8, want_gt=True)
+    assert s == osts == [0] * 64
+    want = G.batch_gt([B.f12_from_bytes(x) for x in lhs], [G.batch_r(sr[16 * q:16 * q + 16]) for q in range(64)])
+    assert g == B.f12_to_bytes(want)
+
+
+def test_config3_many_non_subgroup_b(workload3, cpu):
+    """5% of the 65,536 proofs carry a B on the twist but outside G2: the deferred G2 check in the
+    R-chain turns each DECODE_INVALID (Proof::read) while K4 and the VK-side root work already ran
+    on the side stream -- the gated recompute must give exactly the reference's statuses"""
+    from zebra_amd import Context
+    proofs, kinds, inputs, _ = workload3
+    pts = load_golden("points.json")
+    bad_b = bytes.fromhex(pts["g2_not_in_subgroup"])
+    pr = bytearray(proofs)
+    bad = list(range(7, 65536, 20))
+    for i in bad:
+        pr[192 * i + 48:192 * i + 144] = bad_b
+    pr = bytes(pr)
+    want = oracle_statuses(cpu, pr, kinds, inputs, bad[::400])
+    assert set(want.values()) == {1}
+    c = Context(device=0, max_batch=65536)
+    try:
+        sts, _ = c.verify_batch(pr, kinds, inputs)
+        st = c.stats()
+    finally:
+        c.close()
+    assert {i: s for i, s in enumerate(sts) if s} == {i: 1 for i in bad}
+    assert st["b_subgroup_recomputes"] >= 1 and st["bisections"] == 0

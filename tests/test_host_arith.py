@@ -213,3 +213,19 @@ def test_field_products_host_edges(L, field):
         fn(field, x.to_bytes(w, "little"), y.to_bytes(w, "little"), out)
         got.append(out.raw)
     assert not TF.mismatches(field, pairs, got)
+
+
+def test_lines_lane_equals_g2_prepared(L):
+    """the straight-line R-chain steps of zg_lines.h (k_batch_lines_lane) give exactly the scaled
+    G2Prepared lines of pairing's doubling_step / addition_step (zg_pairing.h g2_prepare + ell's
+    px / py scaling), all 68 triples, for random B in G2 and P in G1"""
+    import ctypes
+    rng = random.Random(31)
+    for _ in range(3):
+        q = B.ec_mul(B.FQ2, B.G2_GEN, rng.randrange(1, B.R))
+        p = B.ec_mul(B.FQ, B.G1_GEN, rng.randrange(1, B.R))
+        qb = b"".join(fq_b(v) for v in (q[0][0], q[0][1], q[1][0], q[1][1]))
+        pb = fq_b(p[0]) + fq_b(p[1])
+        a, r = ctypes.create_string_buffer(68 * 3 * 96), ctypes.create_string_buffer(68 * 3 * 96)
+        L.zgt_lines_lane(qb, pb, a, r)
+        assert a.raw == r.raw

@@ -27,6 +27,11 @@ for s in $STEPS; do
     python3 -c "import json; d=json.load(open('$O/bench_quick.json')); print('64k', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
     timeout -k 10 200 python -u bench.py --no-cpu --no-configs --proofs 8192 > $O/bench_8192.json 2> $O/bench_8192.err || { echo "bench 8192 failed"; tail -30 $O/bench_8192.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_8192.json')); print('8k', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')" ;;
+  lanes)
+    for v in 0 1 2; do
+      ZG_LINES_LANE=$v timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_lanes$v.json 2> $O/bench_lanes$v.err || { echo "bench lanes $v failed"; tail -30 $O/bench_lanes$v.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench_lanes$v.json')); print('lines_lane $v', round(d['value']), round(d['ms_per_step'],3), {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
+    done ;;
   prof)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }

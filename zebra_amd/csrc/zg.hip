@@ -139,6 +139,8 @@ struct zg_ctx {
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
+  int lines_lane = 1;       // ZG_LINES_LANE: the straight-line R-chain (zg_lines.hip) sized for 2 waves
+                            // per SIMD (1) or 1 (2); 0 the staged program (zg_kernels.h)
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
@@ -258,6 +260,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
+  if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
   if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
   if (const char* e = getenv("ZG_DEBUG_EACH")) ctx->debug_each = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
@@ -282,12 +285,12 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
   A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
   A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
-  A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT));
-  A(dalloc(&ctx->msm.start, ZG_MSM_NCOUNT + 1));
-  A(dalloc(&ctx->msm.cursor, ZG_MSM_NCOUNT));
-  A(dalloc(&ctx->msm.entries, 2 * (size_t)cap * ZG_MSM_W));
-  A(dalloc(&ctx->msm.bsum, (size_t)ZG_MSM_NCOUNT * ZG_MSM_PARTS));
-  A(dalloc(&ctx->msm.wsum, ZG_MSM_GROUPS));
+  A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT_MAX));
+  A(dalloc(&ctx->msm.start, ZG_MSM_NCOUNT_MAX + 1));
+  A(dalloc(&ctx->msm.cursor, ZG_MSM_NCOUNT_MAX));
+  A(dalloc(&ctx->msm.entries, 2 * (size_t)cap * ZG_MSM_WMAX));
+  A(dalloc(&ctx->msm.seg, (size_t)ZG_MSM_GROUPS_MAX * ZG_MSM_SEG_MAX * 2));
+  A(dalloc(&ctx->msm.wsum, ZG_MSM_GROUPS_MAX));
   A(dalloc(&ctx->msm.frpart, ((size_t)cap / ZG_FR_CHUNK + 1) * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->d_nodes, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_msm, (size_t)ZG_NODE_CHUNK * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS));
@@ -299,7 +302,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   // surface a broken device / stream now rather than inside a later batch
   A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
   A(hipMemsetAsync(ctx->d_int, 0, sizeof(int) * 16, ctx->side));
-  A(hipMemsetAsync(ctx->msm.entries, 0, sizeof(uint32_t) * 2 * (size_t)cap * ZG_MSM_W, ctx->side));
+  A(hipMemsetAsync(ctx->msm.entries, 0, sizeof(uint32_t) * 2 * (size_t)cap * ZG_MSM_WMAX, ctx->side));
   A(hipStreamSynchronize(ctx->stream));
   A(hipStreamSynchronize(ctx->side));
   if (e != hipSuccess) {
@@ -323,7 +326,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
-                  ctx->msm.entries, ctx->msm.bsum, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
+                  ctx->msm.entries, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
                   ctx->d_dbg};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -660,9 +663,10 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 
 namespace zg {
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);          // zg_decode.hip
-hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate,
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate,
                            hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr);          // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
+hipError_t launch_lines_lane(unsigned groups, hipStream_t st, const BatchBufs& b, Fq2* lines, int wpe);  // zg_lines.hip
 hipError_t launch_jj_comb(hipStream_t st, uint32_t* table);                                    // zg_jubjub.hip
 hipError_t launch_redjubjub(hipStream_t st, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                             const uint8_t* gen, int n, const uint32_t* comb, uint8_t* ok);
@@ -731,8 +735,12 @@ static int run_pipeline(zg_ctx* ctx) {
     hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
                        (const Fq2*)ctx->d_lines, (const int*)b.bfail);  // no-op unless bfail / wait failure
   } else {
-    hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
-    HIPCHK(hipGetLastError());
+    if (ctx->lines_lane) {  // lane = proof, straight-line products (zg_lines.hip)
+      HIPCHK(launch_lines_lane(groups, ctx->stream, b, ctx->d_lines, ctx->lines_lane == 2 ? 1 : 2));
+    } else {                // staged program, lane = proof, wave = product (zg_kernels.h)
+      hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     if (quads)
       hipLaunchKernelGGL(k_batch_fchain4, dim3((unsigned)((ctx->npad / 4 + 63) / 64)), dim3(64 * ZG_FC_NW), 0,
@@ -907,7 +915,8 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
 static int collect_batch_stats(zg_ctx* ctx) {
   int flags[2] = {0, 0}, entries = 0;
   HIPCHK(hipMemcpyAsync(flags, ctx->d_int + 8, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipMemcpyAsync(&entries, ctx->msm.start + ZG_MSM_NCOUNT, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(&entries, ctx->msm.start + msm_shape(ctx->npad).ncount(), sizeof(int),
+                        hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   ctx->stats[0]++;

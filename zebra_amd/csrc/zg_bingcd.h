@@ -217,4 +217,14 @@ ZG_INL Fr fr_inv_vt(const Fr& a) {
   return fr_mul(fp_inv_vt<FrM, ZG_INV_T_FR>(a), r3);
 }
 
+// Montgomery-form inverse of a Montgomery-form Fq: a fixed number of branch-free steps whatever
+// the value (every lane of a wave runs the same instruction stream), so it also serves values
+// derived from the secret batch scalars (the affine r_i A_i of the decode kernel).
+ZG_NOINL inline Fq fq_inv(Fq a) {
+  Fq r3;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r3.l[i] = FQ_R3[i];
+  return fq_mul(fp_inv_vt<FqM, ZG_INV_T_FQ>(a), r3);
+}
+
 }  // namespace zg

@@ -286,7 +286,7 @@ __device__ void coop_inv(CoopWS* ws, int dst, int a) {
     Fq2 c1 = f2_sub(f2_mul_nr(f2_sqr(t.c2)), f2_mul(t.c0, t.c1));
     Fq2 c2 = f2_sub(f2_sqr(t.c1), f2_mul(t.c0, t.c2));
     Fq2 n = f2_add(f2_mul(t.c0, c0), f2_mul_nr(f2_add(f2_mul(t.c2, c1), f2_mul(t.c1, c2))));
-    Fq ni = fq_inv_vartime(fq_add(fq_sqr(n.c0), fq_sqr(n.c1)));
+    Fq ni = fq_inv(fq_add(fq_sqr(n.c0), fq_sqr(n.c1)));
     Fq2 nin = {fq_mul(n.c0, ni), fq_neg(fq_mul(n.c1, ni))};
     Fq6 ti = {f2_mul(c0, nin), f2_mul(c1, nin), f2_mul(c2, nin)};
     Fq12 r = {f6_mul(f.c0, ti), f6_neg(f6_mul(f.c1, ti))};

@@ -6,21 +6,25 @@
 // sum_i r_i C_i. r_i = k0 + k1 lambda (zg_groth16.h), so the sum is an MSM over the 2N points
 // {C_i, sigma(C_i)} with scalars {k0_i (65 bits), k1_i (64 bits)}, sigma(x, y) = (beta x, y).
 //
-// Signed-digit buckets, c = 11 bits per window, 6 windows (66 bits), 1024 buckets per
-// (key, window): digit d in [-1023, 1024] puts +-P into bucket |d| - 1.
+// Signed-digit buckets: c bits per window, W windows (c W >= 66), 2^(c-1) buckets per
+// (key, window); digit d in [-(2^(c-1) - 1), 2^(c-1)] puts +-P into bucket |d| - 1. The window
+// width follows the shard (msm_shape): c = 11 from 32k padded proofs, 10 from 8k, 9 below, so a
+// small shard does not pay for 18,432 buckets.
 //   k_msm_count    lane per (proof, point): bucket sizes (atomic counters)
-//   k_msm_scan     one block: exclusive scan of the 18,432 counters -> bucket offsets
+//   k_msm_scan     one block: exclusive scan of the counters -> bucket offsets
 //   k_msm_scatter  lane per (proof, point): 4-byte entries (proof, sigma?, sign) into buckets
-//   k_msm_bucket   ZG_MSM_PARTS lanes per bucket: each sums a contiguous quarter of its
-//                  entries with mixed Jacobian + affine additions (the bucket phase: entries
-//                  and affine C_i streamed from HBM / L2, partial sums written once)
-//   k_msm_window   a 512-lane block per (key, window): sum_b (b + 1) S_b as local running
-//                  sums + an LDS suffix scan + an LDS tree reduction (wavefront/LDS-level, no
-//                  atomics on points)
-//   k_msm_final    per key: sum_w 2^(11 w) W_w (Horner) -> the C-sum root node ctree[1]
+//   k_msm_bucket   the bucket phase and the first reduction level in one pass: a wave holds
+//                  64/P consecutive buckets of one (key, window), P lanes per bucket; each lane
+//                  sums its share of the bucket's entries (mixed Jacobian + affine additions,
+//                  entries and affine C_i streamed from HBM / L2), the P parts merge in LDS,
+//                  then the wave forms its segment's T = sum_j (j + 1) S_j and U = sum_j S_j by
+//                  an LDS suffix scan and an LDS tree (wavefront-level, no atomics on points)
+//   k_msm_group    a wave per (key, window): sum_s (T_s + 64/P s U_s) over the group's segments
+//                  (suffix scan of U, doublings by 64/P, tree) -> the window sum
+//   k_msm_final    per key: sum_w 2^(c w) W_w (Horner) -> the C-sum root node ctree[1]
 //   k_fr_root / k_fr_final  the root Fr sums S_k0 = sum r_i, S_kj = sum r_i x_ij per key
 // The random batch scalars are secret and uniform, so bucket sizes are Poisson whatever the
-// proofs: ~2N/1024 entries per bucket and key. Per-proof r_i C_i (GLV) and the full C / Fr
+// proofs: ~2N/2^(c-1) entries per bucket and key. Per-proof r_i C_i (GLV) and the full C / Fr
 // trees exist only for bisection (k_c_leaves, then the k_tree_cs levels).
 #pragma once
 #include "zg_batch.h"
@@ -28,24 +32,38 @@
 
 namespace zg {
 
-#define ZG_MSM_C 11
-#define ZG_MSM_W 6
-#define ZG_MSM_NB 1024
-#define ZG_MSM_PARTS 4
-#define ZG_MSM_GROUPS (ZG_NKINDS * ZG_MSM_W)
-#define ZG_MSM_NCOUNT (ZG_MSM_GROUPS * ZG_MSM_NB)
-#define ZG_MSM_WT 512       // lanes of the window-reduction block (2 buckets each)
-#define ZG_MSM_SCAN_T 1024  // lanes of the scan block (18 counters each)
-#define ZG_FR_CHUNK 4096    // proofs per k_fr_root block
+#define ZG_MSM_WMAX 8                              // windows at c = 9
+#define ZG_MSM_NCOUNT_MAX (ZG_NKINDS * 6 * 1024)   // the most buckets over the shapes (c = 11)
+#define ZG_MSM_GROUPS_MAX (ZG_NKINDS * ZG_MSM_WMAX)
+#define ZG_MSM_SEG_MAX 64                          // segments (waves) per (key, window)
+#define ZG_MSM_BT 256                              // threads per k_msm_bucket block (4 waves)
+#define ZG_MSM_SCAN_T 1024                         // lanes of the scan block
+#define ZG_FR_CHUNK 4096                           // proofs per k_fr_root block
+
+// the window shape of a batch of npad (padded) proofs: c bits, w windows, nb = 2^(c-1) buckets
+// per (key, window), parts = lanes per bucket in the bucket phase
+struct MsmShape {
+  int c, w, nb, parts;
+  ZG_HD int groups() const { return ZG_NKINDS * w; }
+  ZG_HD int ncount() const { return groups() * nb; }
+  ZG_HD int bs() const { return 64 / parts; }            // buckets per wave (segment)
+  ZG_HD int nseg() const { return nb / bs(); }           // segments per group
+};
+ZG_HD inline MsmShape msm_shape(size_t npad) {
+  if (npad >= 32768) return {11, 6, 1024, 4};
+  if (npad >= 8192) return {10, 7, 512, 2};
+  return {9, 8, 256, 1};
+}
 
 struct MsmBufs {
-  int* count;          // ZG_MSM_NCOUNT
-  int* start;          // ZG_MSM_NCOUNT + 1
-  int* cursor;         // ZG_MSM_NCOUNT
-  uint32_t* entries;   // 2 x cap x ZG_MSM_W: (proof << 2) | (sigma << 1) | negate
-  G1J* bsum;           // ZG_MSM_NCOUNT x ZG_MSM_PARTS
-  G1J* wsum;           // ZG_MSM_GROUPS
+  int* count;          // ZG_MSM_NCOUNT_MAX
+  int* start;          // ZG_MSM_NCOUNT_MAX + 1
+  int* cursor;         // ZG_MSM_NCOUNT_MAX
+  uint32_t* entries;   // 2 x cap x ZG_MSM_WMAX: (proof << 2) | (sigma << 1) | negate
+  G1J* seg;            // ZG_MSM_GROUPS_MAX x ZG_MSM_SEG_MAX x 2: (T, U) per segment
+  G1J* wsum;           // ZG_MSM_GROUPS_MAX
   Fr* frpart;          // (cap / ZG_FR_CHUNK + 1) x 3 kinds x ZG_MAX_IC
+  MsmShape s;          // this batch's shape (set by launch_msm_root)
 };
 
 }  // namespace zg

@@ -7,15 +7,15 @@
 
 namespace zg {
 
-// window w (11 bits) of the 66-bit scalar lo + 2^64 hi, as a signed digit with carry
-ZG_INL int msm_digit(uint64_t lo, uint32_t hi, int w, int* carry) {
-  const int sh = ZG_MSM_C * w;
-  uint64_t v = sh < 64 ? lo >> sh : 0;
-  if (sh + ZG_MSM_C > 64) v |= (uint64_t)hi << (64 - sh);
-  int t = (int)(v & ((1u << ZG_MSM_C) - 1)) + *carry;
-  if (t > (1 << (ZG_MSM_C - 1))) {
+// window w (c bits) of the 66-bit scalar lo + 2^64 hi, as a signed digit with carry
+ZG_INL int msm_digit(uint64_t lo, uint32_t hi, int c, int w, int* carry) {
+  const int sh = c * w;  // < 64 for every shape (c (W - 1) <= 63)
+  uint64_t v = lo >> sh;
+  if (sh + c > 64) v |= (uint64_t)hi << (64 - sh);
+  int t = (int)(v & ((1u << c) - 1)) + *carry;
+  if (t > (1 << (c - 1))) {
     *carry = 1;
-    return t - (1 << ZG_MSM_C);
+    return t - (1 << c);
   }
   *carry = 0;
   return t;
@@ -36,27 +36,28 @@ __global__ void __launch_bounds__(64) k_msm_count(BatchBufs b, MsmBufs m, const 
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = t >> 1, j = t & 1;
   if (i >= b.npad || !msm_live(b, i)) return;
+  const MsmShape S = m.s;
   const int kind = b.kinds[i];
   uint64_t lo;
   uint32_t hi;
   msm_scalar(b, i, j, &lo, &hi);
   int carry = 0;
-  for (int w = 0; w < ZG_MSM_W; w++) {
-    const int d = msm_digit(lo, hi, w, &carry);
-    if (d) atomicAdd(&m.count[(kind * ZG_MSM_W + w) * ZG_MSM_NB + (d < 0 ? -d : d) - 1], 1);
+  for (int w = 0; w < S.w; w++) {
+    const int d = msm_digit(lo, hi, S.c, w, &carry);
+    if (d) atomicAdd(&m.count[(kind * S.w + w) * S.nb + (d < 0 ? -d : d) - 1], 1);
   }
 }
 
 __global__ void __launch_bounds__(ZG_MSM_SCAN_T) k_msm_scan(MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  constexpr int PER = ZG_MSM_NCOUNT / ZG_MSM_SCAN_T;
-  static_assert(PER * ZG_MSM_SCAN_T == ZG_MSM_NCOUNT, "scan tiling");
+  constexpr int PER = ZG_MSM_NCOUNT_MAX / ZG_MSM_SCAN_T;
+  static_assert(PER * ZG_MSM_SCAN_T == ZG_MSM_NCOUNT_MAX, "scan tiling");
   __shared__ int sh[ZG_MSM_SCAN_T];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, nc = m.s.ncount();
   int c[PER], s = 0;
 #pragma unroll
   for (int q = 0; q < PER; q++) {
-    c[q] = m.count[t * PER + q];
+    c[q] = t * PER + q < nc ? m.count[t * PER + q] : 0;
     s += c[q];
   }
   sh[t] = s;
@@ -70,11 +71,13 @@ __global__ void __launch_bounds__(ZG_MSM_SCAN_T) k_msm_scan(MsmBufs m, const int
   int off = sh[t] - s;
 #pragma unroll
   for (int q = 0; q < PER; q++) {
-    m.start[t * PER + q] = off;
-    m.cursor[t * PER + q] = off;
+    if (t * PER + q < nc) {
+      m.start[t * PER + q] = off;
+      m.cursor[t * PER + q] = off;
+    }
     off += c[q];
   }
-  if (t == ZG_MSM_SCAN_T - 1) m.start[ZG_MSM_NCOUNT] = off;
+  if (t == ZG_MSM_SCAN_T - 1) m.start[nc] = off;
 }
 
 __global__ void __launch_bounds__(64) k_msm_scatter(BatchBufs b, MsmBufs m, const int* gate) {
@@ -82,88 +85,136 @@ __global__ void __launch_bounds__(64) k_msm_scatter(BatchBufs b, MsmBufs m, cons
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = t >> 1, j = t & 1;
   if (i >= b.npad || !msm_live(b, i)) return;
+  const MsmShape S = m.s;
   const int kind = b.kinds[i];
   uint64_t lo;
   uint32_t hi;
   msm_scalar(b, i, j, &lo, &hi);
   int carry = 0;
-  for (int w = 0; w < ZG_MSM_W; w++) {
-    const int d = msm_digit(lo, hi, w, &carry);
+  for (int w = 0; w < S.w; w++) {
+    const int d = msm_digit(lo, hi, S.c, w, &carry);
     if (!d) continue;
-    const int pos = atomicAdd(&m.cursor[(kind * ZG_MSM_W + w) * ZG_MSM_NB + (d < 0 ? -d : d) - 1], 1);
+    const int pos = atomicAdd(&m.cursor[(kind * S.w + w) * S.nb + (d < 0 ? -d : d) - 1], 1);
     m.entries[pos] = ((uint32_t)i << 2) | ((uint32_t)j << 1) | (d < 0 ? 1u : 0u);
   }
 }
 
-__global__ void __launch_bounds__(64) k_msm_bucket(BatchBufs b, MsmBufs m, const int* gate) {
+// The bucket phase with the first reduction level (see zg_msm.h). Wave gw of the grid holds
+// buckets [gw BS, (gw + 1) BS) (BS = 64 / P, inside one (key, window) group), lane = (bucket j,
+// part); the segment's outputs are T = sum_j (j + 1) S_j and U = sum_j S_j.
+__global__ void __launch_bounds__(ZG_MSM_BT) k_msm_bucket(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ZG_MSM_NCOUNT * ZG_MSM_PARTS) return;
-  const int bucket = t / ZG_MSM_PARTS, part = t % ZG_MSM_PARTS;
-  const int lo = m.start[bucket], len = m.start[bucket + 1] - lo;
-  const int beg = lo + len * part / ZG_MSM_PARTS, end = lo + len * (part + 1) / ZG_MSM_PARTS;
-  const Fq beta = fq_const(G1_BETA);
+  __shared__ G1J sh[ZG_MSM_BT];
+  const MsmShape S = m.s;
+  const int lane = threadIdx.x & 63, w0 = threadIdx.x & ~63;
+  const int gw = blockIdx.x * (ZG_MSM_BT / 64) + (threadIdx.x >> 6);
+  const int P = S.parts, BS = S.bs();
+  const bool live = gw * BS < S.ncount();  // whole waves are live or not
+  const int j = lane / P, part = lane % P;
   G1J acc = jac_infinity<Fq>();
-  for (int e = beg; e < end; e++) {
-    const uint32_t ent = m.entries[e];
-    // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
-    // status between count and scatter -- then bfail > 0 and the gated recompute redoes it;
-    // it must still stay inside the buffers)
-    if ((ent >> 2) >= (uint32_t)b.npad) continue;
-    const G1A c = b.ptAC[(size_t)b.npad + (ent >> 2)];
-    const Fq x = (ent & 2u) ? fq_mul(c.x, beta) : c.x;
-    const Fq y = (ent & 1u) ? fq_neg(c.y) : c.y;
-    acc = jac_add_aff_inl(acc, G1A{x, y, false});
+  if (live) {
+    const int bucket = gw * BS + j;
+    const int lo = m.start[bucket], len = m.start[bucket + 1] - lo;
+    const int beg = lo + len * part / P, end = lo + len * (part + 1) / P;
+    const Fq beta = fq_const(G1_BETA);
+    for (int e = beg; e < end; e++) {
+      const uint32_t ent = m.entries[e];
+      // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
+      // status between count and scatter -- then bfail > 0 and the gated recompute redoes it;
+      // it must still stay inside the buffers)
+      if ((ent >> 2) >= (uint32_t)b.npad) continue;
+      const G1A c = b.ptAC[(size_t)b.npad + (ent >> 2)];
+      const Fq x = (ent & 2u) ? fq_mul(c.x, beta) : c.x;
+      const Fq y = (ent & 1u) ? fq_neg(c.y) : c.y;
+      acc = jac_add_aff_inl(acc, G1A{x, y, false});
+    }
   }
-  m.bsum[t] = acc;
+  // merge the P parts of each bucket: S_j lands in lane j P
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int d = 1; d < P; d <<= 1) {
+    G1J v = sh[threadIdx.x];
+    if (part % (2 * d) == 0) v = jac_add_full(v, sh[threadIdx.x + d]);
+    __syncthreads();
+    sh[threadIdx.x] = v;
+    __syncthreads();
+  }
+  // compact: lane j < BS holds S_j
+  G1J v = lane < BS ? sh[w0 + lane * P] : jac_infinity<Fq>();
+  __syncthreads();
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  // suffix sums H_j = sum_{j' >= j} S_j' (inclusive Hillis-Steele, BS lanes)
+  for (int d = 1; d < BS; d <<= 1) {
+    G1J u = sh[threadIdx.x];
+    if (lane + d < BS) u = jac_add_full(u, sh[threadIdx.x + d]);
+    __syncthreads();
+    sh[threadIdx.x] = u;
+    __syncthreads();
+  }
+  const G1J U = sh[w0];  // H_0
+  // T = sum_j H_j: tree over the BS suffix sums
+  for (int d = BS / 2; d >= 1; d >>= 1) {
+    G1J u = sh[threadIdx.x];
+    if (lane < d) u = jac_add_full(u, sh[threadIdx.x + d]);
+    __syncthreads();
+    sh[threadIdx.x] = u;
+    __syncthreads();
+  }
+  if (live && lane == 0) {
+    const int g = gw / S.nseg(), s = gw % S.nseg();
+    m.seg[((size_t)g * ZG_MSM_SEG_MAX + s) * 2 + 0] = sh[w0];
+    m.seg[((size_t)g * ZG_MSM_SEG_MAX + s) * 2 + 1] = U;
+  }
 }
 
-// sum_{b < 1024} (b + 1) S_b of one (key, window). Lane t holds buckets 2t, 2t + 1:
-// a_t = S_2t + 2 S_2t+1, R_t = S_2t + S_2t+1; sum = sum_t a_t + 2 sum_{t >= 1} H_t with the
-// suffix sums H_t = sum_{t' >= t} R_t' (an LDS scan), then an LDS tree reduction.
-__global__ void __launch_bounds__(ZG_MSM_WT) k_msm_window(MsmBufs m, const int* gate) {
+// one wave per (key, window) group: sum_b (b + 1) S_b = sum_s (T_s + BS s U_s), with
+// sum_s s U_s = sum_{s >= 1} H_s, H_s = sum_{s' >= s} U_s' (lane s = segment s)
+__global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  static_assert(2 * ZG_MSM_WT == ZG_MSM_NB, "two buckets per lane");
-  __shared__ G1J sh[ZG_MSM_WT];
-  const int g = blockIdx.x, t = threadIdx.x;
-  const G1J* bs = m.bsum + ((size_t)g * ZG_MSM_NB + 2 * t) * ZG_MSM_PARTS;
-  G1J s0 = bs[0], s1 = bs[ZG_MSM_PARTS];
-  for (int p = 1; p < ZG_MSM_PARTS; p++) {
-    s0 = jac_add_full(s0, bs[p]);
-    s1 = jac_add_full(s1, bs[ZG_MSM_PARTS + p]);
-  }
-  const G1J R = jac_add_full(s0, s1);
-  const G1J a = jac_add_full(R, s1);
-  sh[t] = R;
+  __shared__ G1J sh[64];
+  const MsmShape S = m.s;
+  const int g = blockIdx.x, s = threadIdx.x, ns = S.nseg();
+  const G1J* sg = m.seg + (size_t)g * ZG_MSM_SEG_MAX * 2;
+  const G1J T = s < ns ? sg[2 * s] : jac_infinity<Fq>();
+  sh[s] = s < ns ? sg[2 * s + 1] : jac_infinity<Fq>();
   __syncthreads();
-  for (int d = 1; d < ZG_MSM_WT; d <<= 1) {  // inclusive suffix scan
-    G1J v = sh[t];
-    if (t + d < ZG_MSM_WT) v = jac_add_full(v, sh[t + d]);
+  for (int d = 1; d < ns; d <<= 1) {
+    G1J u = sh[s];
+    if (s + d < ns) u = jac_add_full(u, sh[s + d]);
     __syncthreads();
-    sh[t] = v;
+    sh[s] = u;
     __syncthreads();
   }
-  G1J v = a;
-  if (t >= 1) v = jac_add_full(v, jac_dbl_inl(sh[t]));
+  G1J x = T;
+  if (s >= 1 && s < ns) {
+    G1J h = sh[s];
+    for (int q = S.bs(); q > 1; q >>= 1) h = jac_dbl_inl(h);  // BS = 2^k
+    x = jac_add_full(x, h);
+  }
   __syncthreads();
-  sh[t] = v;
+  sh[s] = x;
   __syncthreads();
-  for (int s = ZG_MSM_WT / 2; s >= 1; s >>= 1) {
-    if (t < s) sh[t] = jac_add_full(sh[t], sh[t + s]);
+  for (int d = 32; d >= 1; d >>= 1) {
+    G1J u = sh[s];
+    if (s < d) u = jac_add_full(u, sh[s + d]);
+    __syncthreads();
+    sh[s] = u;
     __syncthreads();
   }
-  if (t == 0) m.wsum[g] = sh[0];
+  if (s == 0) m.wsum[g] = sh[0];
 }
 
-// per key: sum_w 2^(11 w) W_w -> the root node of the C-sum tree (node 1)
+// per key: sum_w 2^(c w) W_w -> the root node of the C-sum tree (node 1)
 __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
   const int kind = threadIdx.x;
   if (kind >= ZG_NKINDS) return;
-  G1J acc = m.wsum[kind * ZG_MSM_W + ZG_MSM_W - 1];
-  for (int w = ZG_MSM_W - 2; w >= 0; w--) {
-    for (int q = 0; q < ZG_MSM_C; q++) acc = jac_dbl_inl(acc);
-    acc = jac_add_full(acc, m.wsum[kind * ZG_MSM_W + w]);
+  const MsmShape S = m.s;
+  G1J acc = m.wsum[kind * S.w + S.w - 1];
+  for (int w = S.w - 2; w >= 0; w--) {
+    for (int q = 0; q < S.c; q++) acc = jac_dbl_inl(acc);
+    acc = jac_add_full(acc, m.wsum[kind * S.w + w]);
   }
   b.ctree[1 * ZG_NKINDS + kind] = acc;
 }
@@ -219,18 +270,21 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
 
 // the batch root's C sums (ctree node 1) and Fr sums (stree node 1) from the decoded batch;
 // gate: null = always, else only if *gate != 0 (the recompute after a deferred B failure)
-hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, const MsmBufs& m, const int* gate, hipEvent_t bucket0,
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate, hipEvent_t bucket0,
                            hipEvent_t bucket1) {
+  m.s = msm_shape(b.npad);
   const unsigned pts = (unsigned)((2 * (size_t)b.npad + 63) / 64);
-  hipError_t e = hipMemsetAsync(m.count, 0, sizeof(int) * ZG_MSM_NCOUNT, st);
+  hipError_t e = hipMemsetAsync(m.count, 0, sizeof(int) * m.s.ncount(), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_msm_count, dim3(pts), dim3(64), 0, st, b, m, gate);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(ZG_MSM_SCAN_T), 0, st, m, gate);
   hipLaunchKernelGGL(k_msm_scatter, dim3(pts), dim3(64), 0, st, b, m, gate);
   if (bucket0 && (e = hipEventRecord(bucket0, st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_bucket, dim3((ZG_MSM_NCOUNT * ZG_MSM_PARTS + 63) / 64), dim3(64), 0, st, b, m, gate);
+  const int waves = m.s.ncount() / m.s.bs();
+  hipLaunchKernelGGL(k_msm_bucket, dim3((waves + ZG_MSM_BT / 64 - 1) / (ZG_MSM_BT / 64)), dim3(ZG_MSM_BT), 0, st, b,
+                     m, gate);
   if (bucket1 && (e = hipEventRecord(bucket1, st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_window, dim3(ZG_MSM_GROUPS), dim3(ZG_MSM_WT), 0, st, m, gate);
+  hipLaunchKernelGGL(k_msm_group, dim3(m.s.groups()), dim3(64), 0, st, m, gate);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, b, m, gate);
   const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;
   hipLaunchKernelGGL(k_fr_root, dim3(nchunks), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, gate);

@@ -6,7 +6,7 @@
 // Products use Karatsuba at every level (Fq2 mul = 3 Fq mul, Fq6 mul = 6 Fq2 mul,
 // Fq12 mul = 3 Fq6 mul = 54 Fq mul). Sparse line products (mul_by_014) cost 13 Fq2 mul.
 #pragma once
-#include "zg_field.h"
+#include "zg_bingcd.h"  // fq_inv (includes zg_field.h)
 
 namespace zg {
 
