@@ -105,3 +105,51 @@ def test_batches_in_flight_match_sequential():
     finally:
         for c in cs:
             c.close()
+
+
+# ---- the two R-chain kernels: the staged program (k_batch_lines) and the straight-line
+# lane-per-proof kernel (zg_lines.hip k_batch_lines_lane, the default from 32k padded proofs),
+# forced through ZG_LINES_LANE at small sizes; ZG_LINES_FCHAIN=0 keeps the split launches
+def make_lines_ctx(lane):
+    from zebra_amd import Context
+    saved = {k: os.environ.get(k) for k in ("ZG_LINES_LANE", "ZG_LINES_FCHAIN")}
+    os.environ["ZG_LINES_LANE"] = lane
+    os.environ["ZG_LINES_FCHAIN"] = "0"
+    try:
+        return Context(device=0, max_batch=4096, seed=7)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def lctxs():
+    cs = {m: make_lines_ctx(m) for m in ("0", "1", "2")}
+    yield cs
+    for c in cs.values():
+        c.close()
+
+
+@pytest.mark.parametrize("lane", ["1", "2"])
+def test_lines_lane_batch64_and_corruptions(lctxs, lane):
+    """the straight-line R-chain (both register budgets): batch64's statuses and GT bytes, the
+    corrupted 4,096 (non-subgroup B: its G2 check and the gated recompute), and the same 576-byte
+    Miller partial as the staged program"""
+    b = load_golden("batch64.json")
+    items = b["items"]
+    proofs, kinds, inputs, nin = fx_batch(items)
+    r = b"".join(bytes.fromhex(e["r"]) for e in items)
+    sts, gt = lctxs[lane].verify_batch(proofs, kinds, inputs, nin, r=r, want_gt=True)
+    assert sts == [e["status"] for e in items]
+    assert gt.hex() == b["gt_out"]
+    cp, ck, cx, want = corrupted_4096(lctxs[lane])
+    assert lctxs[lane].verify_batch(cp, ck, cx)[0] == want
+    parts = []
+    for m in ("0", lane):
+        lctxs[m].batch_begin(cp, ck, cx, r=r * 64)
+        parts.append(lctxs[m].batch_partial())
+        lctxs[m].batch_finish(True, len(ck))
+    assert parts[0] == parts[1]

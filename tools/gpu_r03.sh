@@ -32,6 +32,11 @@ for s in $STEPS; do
       ZG_LINES_LANE=$v timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_lanes$v.json 2> $O/bench_lanes$v.err || { echo "bench lanes $v failed"; tail -30 $O/bench_lanes$v.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/bench_lanes$v.json')); print('lines_lane $v', round(d['value']), round(d['ms_per_step'],3), {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
     done ;;
+  lanes8k)
+    for n in 8192 16384; do for v in 0 1; do
+      ZG_LINES_LANE=$v timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs $n > $O/bench_l$v_$n.json 2> $O/bench_l$v_$n.err || { echo "bench lanes $v $n failed"; tail -30 $O/bench_l$v_$n.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench_l$v_$n.json')); print('n $n lines_lane $v', round(d['value']), round(d['ms_per_step'],3), {k: round(v,3) for k,v in d['phase_ms'].items()})"
+    done; done ;;
   prof)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }

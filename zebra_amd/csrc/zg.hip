@@ -31,6 +31,8 @@ using namespace zg;
 #define ZG_NSTATS 8
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
+#define ZG_LINES_LANE_MIN 32768  // straight-line R-chain from here (r03: 64k 14.93 -> 14.47 ms per batch in
+                                 // flight; 16k 4.90 -> 5.14 and 8k 3.21 -> 3.63 favour the staged program)
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
 
 namespace zg {  // zg_merkle.hip
@@ -139,8 +141,9 @@ struct zg_ctx {
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
-  int lines_lane = 1;       // ZG_LINES_LANE: the straight-line R-chain (zg_lines.hip) sized for 2 waves
-                            // per SIMD (1) or 1 (2); 0 the staged program (zg_kernels.h)
+  int lines_lane = -1;      // ZG_LINES_LANE: -1 auto (the straight-line R-chain from ZG_LINES_LANE_MIN padded
+                            // proofs, else the staged program), 1 / 2 always straight-line sized for 2 / 1
+                            // waves per SIMD, 0 always the staged program (zg_kernels.h)
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
@@ -735,7 +738,8 @@ static int run_pipeline(zg_ctx* ctx) {
     hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
                        (const Fq2*)ctx->d_lines, (const int*)b.bfail);  // no-op unless bfail / wait failure
   } else {
-    if (ctx->lines_lane) {  // lane = proof, straight-line products (zg_lines.hip)
+    const bool lane = ctx->lines_lane > 0 || (ctx->lines_lane < 0 && ctx->npad >= ZG_LINES_LANE_MIN);
+    if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
       HIPCHK(launch_lines_lane(groups, ctx->stream, b, ctx->d_lines, ctx->lines_lane == 2 ? 1 : 2));
     } else {                // staged program, lane = proof, wave = product (zg_kernels.h)
       hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
