@@ -7,6 +7,7 @@
 #include "../../zebra_amd/csrc/zg_bingcd.h"
 #include "../../zebra_amd/csrc/zg_bn254.h"
 #include "../../zebra_amd/csrc/zg_lines.h"
+#include "../../zebra_amd/csrc/zg_msm.h"
 
 using namespace zg;
 
@@ -14,6 +15,24 @@ static Fq ld_fq(const uint8_t* b) { return fq_to_mont(fq_limbs_from_be(b)); }
 static void st_fq(const Fq& a, uint8_t* b) { fq_limbs_to_be(fq_from_mont(a), b); }
 
 extern "C" {
+
+// K4's signed-digit windows (zg_msm.h msm_shape / msm_digit) of the scalar lo + 2^64 hi for a
+// batch of npad padded proofs: digits[w], shifts[w], widths[w]; returns the window count, or -1
+// when the final carry is not zero; shape[] = c, w, nb, parts
+int zgt_msm_digits(uint64_t lo, uint32_t hi, uint64_t npad, int* digits, int* shifts, int* widths, int* shape) {
+  const MsmShape S = msm_shape((size_t)npad);
+  shape[0] = S.c;
+  shape[1] = S.w;
+  shape[2] = S.nb;
+  shape[3] = S.parts;
+  int carry = 0;
+  for (int w = 0; w < S.w; w++) {
+    digits[w] = msm_digit(lo, hi, S, w, &carry);
+    shifts[w] = S.shift(w);
+    widths[w] = S.width(w);
+  }
+  return carry ? -1 : S.w;
+}
 
 // the R-chain of zg_lines.h (k_batch_lines_lane) for one proof: B (x.c0 x.c1 y.c0 y.c1) and
 // P = r A (x y), 48-byte BE each, canonical -> 68 x 3 scaled line coefficients (Fq2 as c0 || c1,

@@ -6,10 +6,14 @@
 // sum_i r_i C_i. r_i = k0 + k1 lambda (zg_groth16.h), so the sum is an MSM over the 2N points
 // {C_i, sigma(C_i)} with scalars {k0_i (65 bits), k1_i (64 bits)}, sigma(x, y) = (beta x, y).
 //
-// Signed-digit buckets: c bits per window, W windows (c W >= 66), 2^(c-1) buckets per
-// (key, window); digit d in [-(2^(c-1) - 1), 2^(c-1)] puts +-P into bucket |d| - 1. The window
-// width follows the shard (msm_shape): c = 11 from 32k padded proofs, 10 from 8k, 9 below, so a
-// small shard does not pay for 18,432 buckets.
+// Signed-digit buckets: W windows whose widths sum to exactly 66 bits (the 65-bit k0 plus the
+// signed-digit carry): the first K windows are c bits wide, the rest c - 1 (K = 66 - (c - 1) W),
+// 2^(c-1) bucket slots per (key, window); digit d in [-(2^(cw-1) - 1), 2^(cw-1)] puts +-P into
+// bucket |d| - 1. The shape follows the shard (msm_shape): c = 11 x 6 from 32k padded proofs,
+// [10 x 3, 9 x 4] from 8k, [9 x 2, 8 x 6] below, so a small shard does not pay for 18,432
+// buckets. (Round 3 first used c = 10 x 7 and 9 x 8 windows: their top window held only the 6
+// or 3 bits left above bit 60 / 63, so every point of a key landed in 32 or 4 buckets and one
+// lane summed hundreds of entries -- 40 ms bucket phases at 4,096 proofs.)
 //   k_msm_count    lane per (proof, point): bucket sizes (atomic counters)
 //   k_msm_scan     one block: exclusive scan of the counters -> bucket offsets
 //   k_msm_scatter  lane per (proof, point): 4-byte entries (proof, sigma?, sign) into buckets
@@ -21,7 +25,7 @@
 //                  an LDS suffix scan and an LDS tree (wavefront-level, no atomics on points)
 //   k_msm_group    a wave per (key, window): sum_s (T_s + 64/P s U_s) over the group's segments
 //                  (suffix scan of U, doublings by 64/P, tree) -> the window sum
-//   k_msm_final    per key: sum_w 2^(c w) W_w (Horner) -> the C-sum root node ctree[1]
+//   k_msm_final    per key: sum_w 2^shift(w) W_w (Horner) -> the C-sum root node ctree[1]
 //   k_fr_root / k_fr_final  the root Fr sums S_k0 = sum r_i, S_kj = sum r_i x_ij per key
 // The random batch scalars are secret and uniform, so bucket sizes are Poisson whatever the
 // proofs: ~2N/2^(c-1) entries per bucket and key. Per-proof r_i C_i (GLV) and the full C / Fr
@@ -38,12 +42,17 @@ namespace zg {
 #define ZG_MSM_SEG_MAX 64                          // segments (waves) per (key, window)
 #define ZG_MSM_BT 256                              // threads per k_msm_bucket block (4 waves)
 #define ZG_MSM_SCAN_T 1024                         // lanes of the scan block
-#define ZG_FR_CHUNK 4096                           // proofs per k_fr_root block
+#define ZG_FR_CHUNK 256                            // proofs per k_fr_root block (256 blocks at 64k;
+                                                   // r03: 4,096 gave 16 blocks and a 5.3 ms launch)
 
 // the window shape of a batch of npad (padded) proofs: c bits, w windows, nb = 2^(c-1) buckets
 // per (key, window), parts = lanes per bucket in the bucket phase
+#define ZG_MSM_BITS 66
 struct MsmShape {
   int c, w, nb, parts;
+  ZG_HD int wide() const { return ZG_MSM_BITS - (c - 1) * w; }            // windows of c bits
+  ZG_HD int width(int q) const { return q < wide() ? c : c - 1; }         // bits of window q
+  ZG_HD int shift(int q) const { return q * (c - 1) + (q < wide() ? q : wide()); }
   ZG_HD int groups() const { return ZG_NKINDS * w; }
   ZG_HD int ncount() const { return groups() * nb; }
   ZG_HD int bs() const { return 64 / parts; }            // buckets per wave (segment)
@@ -53,6 +62,21 @@ ZG_HD inline MsmShape msm_shape(size_t npad) {
   if (npad >= 32768) return {11, 6, 1024, 4};
   if (npad >= 8192) return {10, 7, 512, 2};
   return {9, 8, 256, 1};
+}
+
+// window w of the 66-bit scalar lo + 2^64 hi (S.width(w) bits from bit S.shift(w)), as a signed
+// digit with carry
+ZG_INL int msm_digit(uint64_t lo, uint32_t hi, const MsmShape& S, int w, int* carry) {
+  const int sh = S.shift(w), c = S.width(w);  // sh <= 66 - (c - 1) < 64 for every shape
+  uint64_t v = lo >> sh;
+  if (sh + c > 64) v |= (uint64_t)hi << (64 - sh);
+  int t = (int)(v & ((1u << c) - 1)) + *carry;
+  if (t > (1 << (c - 1))) {
+    *carry = 1;
+    return t - (1 << c);
+  }
+  *carry = 0;
+  return t;
 }
 
 struct MsmBufs {

@@ -7,20 +7,6 @@
 
 namespace zg {
 
-// window w (c bits) of the 66-bit scalar lo + 2^64 hi, as a signed digit with carry
-ZG_INL int msm_digit(uint64_t lo, uint32_t hi, int c, int w, int* carry) {
-  const int sh = c * w;  // < 64 for every shape (c (W - 1) <= 63)
-  uint64_t v = lo >> sh;
-  if (sh + c > 64) v |= (uint64_t)hi << (64 - sh);
-  int t = (int)(v & ((1u << c) - 1)) + *carry;
-  if (t > (1 << (c - 1))) {
-    *carry = 1;
-    return t - (1 << c);
-  }
-  *carry = 0;
-  return t;
-}
-
 // the scalar of point j of proof i: j = 0 -> k0 = 2a + 1 (65 bits), j = 1 -> k1 = b
 ZG_INL void msm_scalar(const BatchBufs& b, int i, int j, uint64_t* lo, uint32_t* hi) {
   uint64_t ra, rb;
@@ -43,7 +29,7 @@ __global__ void __launch_bounds__(64) k_msm_count(BatchBufs b, MsmBufs m, const 
   msm_scalar(b, i, j, &lo, &hi);
   int carry = 0;
   for (int w = 0; w < S.w; w++) {
-    const int d = msm_digit(lo, hi, S.c, w, &carry);
+    const int d = msm_digit(lo, hi, S, w, &carry);
     if (d) atomicAdd(&m.count[(kind * S.w + w) * S.nb + (d < 0 ? -d : d) - 1], 1);
   }
 }
@@ -92,7 +78,7 @@ __global__ void __launch_bounds__(64) k_msm_scatter(BatchBufs b, MsmBufs m, cons
   msm_scalar(b, i, j, &lo, &hi);
   int carry = 0;
   for (int w = 0; w < S.w; w++) {
-    const int d = msm_digit(lo, hi, S.c, w, &carry);
+    const int d = msm_digit(lo, hi, S, w, &carry);
     if (!d) continue;
     const int pos = atomicAdd(&m.cursor[(kind * S.w + w) * S.nb + (d < 0 ? -d : d) - 1], 1);
     m.entries[pos] = ((uint32_t)i << 2) | ((uint32_t)j << 1) | (d < 0 ? 1u : 0u);
@@ -205,7 +191,7 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
   if (s == 0) m.wsum[g] = sh[0];
 }
 
-// per key: sum_w 2^(c w) W_w -> the root node of the C-sum tree (node 1)
+// per key: sum_w 2^shift(w) W_w -> the root node of the C-sum tree (node 1)
 __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
   const int kind = threadIdx.x;
@@ -213,7 +199,7 @@ __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const 
   const MsmShape S = m.s;
   G1J acc = m.wsum[kind * S.w + S.w - 1];
   for (int w = S.w - 2; w >= 0; w--) {
-    for (int q = 0; q < S.c; q++) acc = jac_dbl_inl(acc);
+    for (int q = 0; q < S.width(w); q++) acc = jac_dbl_inl(acc);  // 2^(shift(w + 1) - shift(w))
     acc = jac_add_full(acc, m.wsum[kind * S.w + w]);
   }
   b.ctree[1 * ZG_NKINDS + kind] = acc;
@@ -241,13 +227,22 @@ __global__ void __launch_bounds__(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G) k_fr_root(Bat
   if (g == 0) m.frpart[(size_t)chunk * KS + ks] = sh[t];
 }
 
-__global__ void __launch_bounds__(64) k_fr_final(BatchBufs b, MsmBufs m, int nchunks, const int* gate) {
+// the chunk partials -> stree node 1: lanes t = 30 g + ks stride over the chunks, then an LDS tree
+__global__ void __launch_bounds__(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G) k_fr_final(BatchBufs b, MsmBufs m, int nchunks,
+                                                                            const int* gate) {
   if (gate && *gate == 0) return;
-  const int ks = threadIdx.x;
-  if (ks >= ZG_NKINDS * ZG_MAX_IC) return;
+  constexpr int KS = ZG_NKINDS * ZG_MAX_IC;
+  __shared__ Fr sh[KS * ZG_FR_G];
+  const int t = threadIdx.x, ks = t % KS, g = t / KS;
   Fr acc = fp_zero<FrM>();
-  for (int c = 0; c < nchunks; c++) acc = fr_add(acc, m.frpart[(size_t)c * ZG_NKINDS * ZG_MAX_IC + ks]);
-  b.stree[(size_t)1 * ZG_NKINDS * ZG_MAX_IC + ks] = acc;
+  for (int c = g; c < nchunks; c += ZG_FR_G) acc = fr_add(acc, m.frpart[(size_t)c * KS + ks]);
+  sh[t] = acc;
+  __syncthreads();
+  for (int s = ZG_FR_G / 2; s >= 1; s >>= 1) {
+    if (g < s) sh[t] = fr_add(sh[t], sh[t + s * KS]);
+    __syncthreads();
+  }
+  if (g == 0) b.stree[(size_t)1 * KS + ks] = sh[t];
 }
 
 // bisection only: the per-proof leaves r_i C_i (GLV) of the C-sum trees, infinity for the other
@@ -288,7 +283,7 @@ hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const 
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, b, m, gate);
   const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;
   hipLaunchKernelGGL(k_fr_root, dim3(nchunks), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, gate);
-  hipLaunchKernelGGL(k_fr_final, dim3(1), dim3(64), 0, st, b, m, nchunks, gate);
+  hipLaunchKernelGGL(k_fr_final, dim3(1), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, nchunks, gate);
   return hipGetLastError();
 }
 
