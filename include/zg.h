@@ -134,7 +134,9 @@ int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t*
  *   zg_batch_partial         this rank's Miller partial F_g (576 B, not final-exponentiated)
  *   zg_gt_check              product of `count` partials, ONE final exponentiation, == 1 ?
  *   zg_batch_finish          statuses; when batch_ok == 0 bisects this rank's shard
- * The *_device variant takes device pointers (HBM-resident inputs; same layouts). */
+ * The *_device variant takes device pointers (HBM-resident inputs; same layouts) and reads them in
+ * place, without a copy: they must stay allocated and unchanged until zg_batch_finish returns
+ * (bisection re-reads them). */
 int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* kinds, const uint8_t* inputs,
                    const uint8_t* n_inputs, const uint8_t* r);
 int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,

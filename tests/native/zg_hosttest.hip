@@ -16,6 +16,29 @@ static void st_fq(const Fq& a, uint8_t* b) { fq_limbs_to_be(fq_from_mont(a), b);
 
 extern "C" {
 
+// G1 subgroup check and GLV product r A in the word form (zg_curve.h / zg_groth16.h) and in lazy
+// digits (zg_fqd.h) for an affine point (x, y: 48-byte BE, canonical, on the curve): res[0..1]
+// the two subgroup verdicts; out_w / out_d the affine [k0 + k1 lambda] P (96 B each, zero bytes
+// for infinity) from the word / digit GLV with k0 = 2a + 1, k1 = b
+void zgt_g1_check_glv(const uint8_t* x, const uint8_t* y, uint64_t a, uint64_t b, int* res, uint8_t* out_w,
+                      uint8_t* out_d) {
+  const G1A p = {ld_fq(x), ld_fq(y), false};
+  res[0] = g1_in_subgroup(p);
+  res[1] = g1_in_subgroup_d(p);
+  const G1A w = jac_to_aff(g1_glv_mul(p, a, b));
+  const G1A d = jac_to_aff(g1_glv_mul_d(p, a, b));
+  memset(out_w, 0, 96);
+  memset(out_d, 0, 96);
+  if (!w.inf) {
+    st_fq(w.x, out_w);
+    st_fq(w.y, out_w + 48);
+  }
+  if (!d.inf) {
+    st_fq(d.x, out_d);
+    st_fq(d.y, out_d + 48);
+  }
+}
+
 // K4's signed-digit windows (zg_msm.h msm_shape / msm_digit) of the scalar lo + 2^64 hi for a
 // batch of npad padded proofs: digits[w], shifts[w], widths[w]; returns the window count, or -1
 // when the final carry is not zero; shape[] = c, w, nb, parts

@@ -253,3 +253,39 @@ def test_msm_windows_cover_the_scalar_evenly():
             assert sum(d[q] << sh[q] for q in range(w)) == k
             assert all(-(1 << (wd[q] - 1)) < d[q] <= 1 << (wd[q] - 1) for q in range(w))
             assert all(abs(d[q]) <= nb for q in range(w))
+
+
+def _g1_points(rng, n):
+    """random G1 points, random curve points outside G1, and the order-3 points (0, +-2)"""
+    pts = [B.ec_mul(B.FQ, B.G1_GEN, rng.randrange(1, B.R)) for _ in range(n)]
+    out = []
+    while len(out) < n:
+        x = rng.randrange(P)
+        rhs = (x * x * x + 4) % P
+        y = pow(rhs, (P + 1) // 4, P)
+        if y * y % P == rhs:
+            out.append((x, y))
+    return [(p, True) for p in pts] + [(p, False) for p in out] + [((0, 2), False), ((0, P - 2), False)]
+
+
+def test_g1_digit_arith_equals_word_form():
+    """the decode kernels' lazy-digit G1 arithmetic (zg_fqd.h: g1_in_subgroup_d, g1_glv_mul_d)
+    against the word form (zg_curve.h / zg_groth16.h) and the oracle: subgroup verdicts on G1
+    points, curve points outside G1 and the order-3 points (0, +-2) (exceptional additions in the
+    chain), and r A for random and extreme GLV scalars"""
+    import ctypes
+    L = hostlib.lib()
+    L.zgt_g1_check_glv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
+                                   ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(7)
+    lam = None
+    for (x, y), ing1 in _g1_points(rng, 6):
+        for a, b in [(rng.getrandbits(64), rng.getrandbits(64)), (0, 0), ((1 << 64) - 1, (1 << 64) - 1),
+                     ((1 << 64) - 1, 0), (0, (1 << 64) - 1)]:
+            res = (ctypes.c_int * 2)()
+            ow, od = ctypes.create_string_buffer(96), ctypes.create_string_buffer(96)
+            L.zgt_g1_check_glv(fq_b(x), fq_b(y), a, b, res, ow, od)
+            assert res[0] == res[1] == int(ing1)
+            assert ow.raw == od.raw
+            if ing1 and a == 0 and b == 0:   # k = 1: r A = A
+                assert ow.raw == fq_b(x) + fq_b(y)

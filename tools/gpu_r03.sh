@@ -42,5 +42,23 @@ for s in $STEPS; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof_bench_iso.json 2> $O/prof_bench_iso.err || { echo "rocprof iso failed"; tail -30 $O/prof_bench_iso.err; exit 1; }
     cd $R && for k in prof prof_iso; do python3 tools/rocpd_stats.py $O/$k/run_results.db $O/kernel_stats_${k#prof}.csv; done ;;
+  variants)
+    for v in $VARIANTS; do
+      ZG_LIB_VARIANT=$v timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_$v.json 2> $O/bench_$v.err || { echo "bench $v failed"; tail -30 $O/bench_$v.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench_$v.json')); print('$v 64k', round(d['value']), round(d['ms_per_step'],3), {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
+    done ;;
+  pghr)
+    for n in 65536 8192; do
+      timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n $n > $O/pghr_$n.json 2> $O/pghr_$n.err || { echo "pghr bench failed"; tail -30 $O/pghr_$n.err; exit 1; }
+      cat $O/pghr_$n.json
+    done
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pghr -o run -- python3 $R/tools/bench_pghr13.py --no-cpu --reps 2 > /dev/null 2> $O/prof_pghr.err || { echo "rocprof pghr failed"; tail -30 $O/prof_pghr.err; exit 1; }
+    cd $R && python3 tools/rocpd_stats.py $O/prof_pghr/run_results.db $O/kernel_stats_pghr.csv && rm -f $O/prof_pghr/run_results.db ;;
+  prof8k)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 36 --warmup 0 > $O/prof8k_bench.json 2> $O/prof8k_bench.err || { echo "rocprof 8k failed"; tail -30 $O/prof8k_bench.err; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8k_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof8k_bench_iso.json 2> $O/prof8k_bench_iso.err || { echo "rocprof 8k iso failed"; tail -30 $O/prof8k_bench_iso.err; exit 1; }
+    cd $R && for k in prof8k prof8k_iso; do python3 tools/rocpd_stats.py $O/$k/run_results.db $O/kernel_stats_${k}.csv; done ;;
   esac
 done

@@ -139,6 +139,9 @@ struct zg_ctx {
   int state = 0;
   size_t n = 0, npad = 0;
   const uint8_t* cur_ninputs = nullptr;  // device pointer or null
+  // this batch's inputs on the device: the context's own buffers (host-buffer calls copy into
+  // them), or the caller's HBM-resident buffers (zg_batch_begin_device: read in place, no copy)
+  const uint8_t *cur_proofs = nullptr, *cur_kinds = nullptr, *cur_inputs = nullptr;
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
   int lines_lane = -1;      // ZG_LINES_LANE: -1 auto (the straight-line R-chain from ZG_LINES_LANE_MIN padded
@@ -633,9 +636,9 @@ static int stage_scalars(zg_ctx* ctx, size_t n) {
 static BatchBufs batch_bufs(zg_ctx* ctx) {
   BatchBufs b;
   b.vks = ctx->d_vk;
-  b.proofs = ctx->d_proofs;
-  b.kinds = ctx->d_kinds;
-  b.inputs = ctx->d_inputs;
+  b.proofs = ctx->cur_proofs;
+  b.kinds = ctx->cur_kinds;
+  b.inputs = ctx->cur_inputs;
   b.ninputs = ctx->cur_ninputs;
   b.r = ctx->d_r;
   b.status = ctx->d_status;
@@ -822,6 +825,9 @@ static int batch_begin_locked(zg_ctx* ctx, size_t n, const uint8_t* proofs, cons
     if (n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, n_inputs, n, hipMemcpyHostToDevice, ctx->stream));
   }
   ctx->cur_ninputs = n_inputs ? ctx->d_ninputs : nullptr;
+  ctx->cur_proofs = ctx->d_proofs;
+  ctx->cur_kinds = ctx->d_kinds;
+  ctx->cur_inputs = ctx->d_inputs;
   if ((rc = run_pipeline(ctx))) return rc;
   set_state(ctx, 1);
   return ZG_OK;
@@ -846,18 +852,19 @@ extern "C" int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs
       // device-resident kinds are not inspected on the host: require every VK loaded
       return fail(ctx, ZG_E_NOVK, "device batches need all three verifying keys loaded");
     }
+  // the inputs are read in place (the caller keeps them unchanged until zg_batch_finish): a
+  // shard already resident in HBM is not copied again
   if (n) {
-    HIPCHK(hipMemcpyAsync(ctx->d_proofs, d_proofs, n * 192, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_kinds, d_kinds, n, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->d_inputs, d_inputs, n * 288, hipMemcpyDeviceToDevice, ctx->stream));
     if (d_r) {
       HIPCHK(hipMemcpyAsync(ctx->d_r, d_r, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
     } else if ((rc = stage_scalars(ctx, n))) {
       return rc;
     }
-    if (d_n_inputs) HIPCHK(hipMemcpyAsync(ctx->d_ninputs, d_n_inputs, n, hipMemcpyDeviceToDevice, ctx->stream));
   }
-  ctx->cur_ninputs = d_n_inputs ? ctx->d_ninputs : nullptr;
+  ctx->cur_ninputs = (const uint8_t*)d_n_inputs;
+  ctx->cur_proofs = (const uint8_t*)d_proofs;
+  ctx->cur_kinds = (const uint8_t*)d_kinds;
+  ctx->cur_inputs = (const uint8_t*)d_inputs;
   if ((rc = run_pipeline(ctx))) return rc;
   set_state(ctx, 1);
   return ZG_OK;
@@ -1097,7 +1104,7 @@ static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool 
     // proof, no batch scalars) on the batch's own device inputs must give the same statuses
     const size_t n = ctx->n;
     hipLaunchKernelGGL(k_verify_single, dim3(nblocks(n)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_vk, (int)n,
-                       ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->cur_ninputs, ctx->d_dbg, nullptr);
+                       ctx->cur_proofs, ctx->cur_kinds, ctx->cur_inputs, ctx->cur_ninputs, ctx->d_dbg, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(st.data(), ctx->d_dbg, n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -7,6 +7,19 @@
 
 namespace zg {
 
+// ZG_DECODE_FQD (default 1): the subgroup checks and GLV products in lazy digits (zg_fqd.h);
+// 0: the word form (zg_curve.h / zg_groth16.h)
+#ifndef ZG_DECODE_FQD
+#define ZG_DECODE_FQD 1
+#endif
+#if ZG_DECODE_FQD
+#define ZG_DEC_SUBGROUP g1_in_subgroup_d
+#define ZG_DEC_GLV g1_glv_mul_d
+#else
+#define ZG_DEC_SUBGROUP g1_in_subgroup
+#define ZG_DEC_GLV g1_glv_mul
+#endif
+
 // K1 + K2 + K3 as three launches.
 //
 // k_decode_sqrt: one wave per (64 proofs, G1 point), blocks alternating A / C of the same 64
@@ -52,14 +65,14 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b
   const G1A p = b.ptAC[(size_t)role * b.npad + i];
   const bool ok = !p.inf;
   if (job == 1) {
-    b.okbits[3 * i + role] = ok && g1_in_subgroup(p);
+    b.okbits[3 * i + role] = ok && ZG_DEC_SUBGROUP(p);
     return;
   }
   uint64_t ra = 0, rb = 0;
   if (ok) batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
   G1A o;
   o.inf = true;
-  if (ok) o = jac_to_aff(g1_glv_mul(p, ra, rb));
+  if (ok) o = jac_to_aff(ZG_DEC_GLV(p, ra, rb));
   b.ptA[i] = o;
 }
 

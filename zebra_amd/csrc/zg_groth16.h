@@ -8,6 +8,7 @@
 // SURVEY.md 8(a) rows a1-a4, a8.
 #pragma once
 #include "zg_pairing.h"
+#include "zg_fqd.h"
 
 namespace zg {
 
@@ -142,6 +143,29 @@ ZG_NOINL inline void g1_glv_mul_p(G1J* out, const G1A* pp, uint64_t a, uint64_t 
 ZG_INL G1J g1_glv_mul(const G1A& p, uint64_t a, uint64_t b) {
   G1J r;
   g1_glv_mul_p(&r, &p, a, b);
+  return r;
+}
+// the same product with the 64 doublings and mixed additions in lazy digits (zg_fqd.h)
+ZG_NOINL inline void g1_glv_mul_d_p(G1J* out, const G1A* pp, uint64_t a, uint64_t b) {
+  const FqD px = fqd_from(pp->x), py = fqd_from(pp->y);
+  const FqD bx = fqd_mul(px, fqd_from(fq_const(G1_BETA2))), ny = fqd_neg2(py);  // < 2p, < 3p
+  uint64_t k1 = b, e = 0;
+  for (int j = 0; j < 64; j++) {
+    const uint64_t ej = k1 & 1u, neg = ((a >> j) & 1u) ^ 1u;
+    e |= ej << j;
+    k1 = (k1 >> 1) + (ej & neg);
+  }
+  const bool etop = k1 & 1u;
+  G1D q = g1d_from_aff(etop ? bx : px, etop ? ny : py);
+  for (int j = 63; j >= 0; j--) {
+    const bool ej = (e >> j) & 1u, neg = !((a >> j) & 1u);
+    q = g1d_add_aff(g1d_dbl(q), ej ? bx : px, (ej != neg) ? ny : py);
+  }
+  *out = g1d_to_jac(q);
+}
+ZG_INL G1J g1_glv_mul_d(const G1A& p, uint64_t a, uint64_t b) {
+  G1J r;
+  g1_glv_mul_d_p(&r, &p, a, b);
   return r;
 }
 

@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
   if (live) {
     uint64_t ra, rb;
     batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
-    b.ctree[leaf * ZG_NKINDS + kind] = g1_glv_mul(b.ptAC[leaf], ra, rb);
+    b.ctree[leaf * ZG_NKINDS + kind] = g1_glv_mul_d(b.ptAC[leaf], ra, rb);
   }
 }
 

@@ -139,14 +139,22 @@ ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s
   return acc;
 }
 
-struct PghrPts {  // per proof, written by k_pghr_prep
+#define ZG_PGHR_DEC 9
+struct PghrPts {  // per proof, written by k_pghr_combine
   BA1 p[ZG_BN_PTS];
   BA2 qb;
 };
 
+// the proof's points as decoded, acc + a and acc + a + c (k_pghr_prep -> k_pghr_rho / k_pghr_combine)
+struct PghrDec {
+  BA1 pt[ZG_PGHR_DEC];  // a, a', b', c, c', k, h, acc + a, acc + a + c
+  BA2 qb;
+};
+
+// lane per proof: Proof::from_raw's decodes and checks, acc = ic0 + sum x_j ic_{j+1} (combs)
 __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* proofs, const uint8_t* inputs,
-                                                   const uint8_t* ninputs, const uint8_t* rho, const BnVK* vk,
-                                                   const uint32_t* comb, PghrPts* pts, uint8_t* status) {
+                                                   const uint8_t* ninputs, const BnVK* vk, const uint32_t* comb,
+                                                   PghrDec* dec, uint8_t* status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* pr = proofs + (size_t)296 * i;
@@ -185,45 +193,102 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* proofs, 
     acc = bn_comb_mul(acc, comb, j + 1, xin + 32 * j, 32);
   }
   const BA1 acca = bj1_to_aff(acc);
-  const uint8_t* r = rho + (size_t)64 * i;  // rho2, rho3, rho4, rho5: 16 LE bytes each
-  uint32_t rw[4][4];
-  for (int q = 0; q < 4; q++)
-    for (int l = 0; l < 4; l++)
-      rw[q][l] = (uint32_t)r[16 * q + 4 * l] | ((uint32_t)r[16 * q + 4 * l + 1] << 8) |
-                 ((uint32_t)r[16 * q + 4 * l + 2] << 16) | ((uint32_t)r[16 * q + 4 * l + 3] << 24);
-  const BA1 aa = ba1_add(acca, a);      // acc + a
-  const BA1 aac = ba1_add(aa, c);       // acc + a + c
-  PghrPts& o = pts[i];
-  o.p[0] = a;
-  // P1' = -(a' + rho2 b' + rho3 c' + rho5 c)
-  BJ1 s = bj1_from(ap);
-  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(bp, rw[0], 128)));
-  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(cp, rw[1], 128)));
-  s = bj1_add_aff(s, bj1_to_aff(bj1_mul(c, rw[3], 128)));
-  o.p[1] = ba1_neg(bj1_to_aff(s));
-  o.p[2] = bj1_to_aff(bj1_mul(c, rw[1], 128));
-  o.p[3] = bj1_to_aff(bj1_mul(k, rw[2], 128));
-  o.p[4] = aac.inf ? aac : ba1_neg(bj1_to_aff(bj1_mul(aac, rw[2], 128)));
-  o.p[5] = ba1_neg(bj1_to_aff(bj1_mul(h, rw[3], 128)));
-  // P7 = rho2 vk.b - rho4 gb1 + rho5 (acc + a)
-  BJ1 t = bj1_inf();
-  t = bn_comb_mul(t, comb, ZG_BN_MAX_IC, r, 16);
-  const BA1 g4 = bj1_to_aff(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 16));
-  t = bj1_add_aff(t, ba1_neg(g4));
-  if (!aa.inf) t = bj1_add_aff(t, bj1_to_aff(bj1_mul(aa, rw[3], 128)));
-  o.p[6] = bj1_to_aff(t);
+  const BA1 aa = ba1_add(acca, a);  // acc + a
+  PghrDec& o = dec[i];
+  o.pt[0] = a;
+  o.pt[1] = ap;
+  o.pt[2] = bp;
+  o.pt[3] = c;
+  o.pt[4] = cp;
+  o.pt[5] = k;
+  o.pt[6] = h;
+  o.pt[7] = aa;
+  o.pt[8] = ba1_add(aa, c);  // acc + a + c
   o.qb = qb;
   status[i] = ZG_STATUS_OK;
 }
 
-// the multi-Miller loop of one proof's 7 pairs -> f
-__global__ void __launch_bounds__(64) k_pghr_miller(int n, const PghrPts* pts, const BLine* lines,
-                                                     const uint8_t* status, Bq12* fout) {
+// the eight 128-bit products rho_j Q of a proof, one per wave of a 512-lane block (64 proofs):
+// wave w computes PGHR_RHO_MUL[w] = (point, rho index), affine, -> mul[8 i + w]. One lane per
+// proof ran them back to back (eight 128-bit double-and-add chains at one wave per SIMD).
+__device__ __constant__ const int8_t PGHR_RHO_MUL[8][2] = {
+    {2, 0},  // rho2 b'
+    {4, 1},  // rho3 c'
+    {3, 3},  // rho5 c
+    {3, 1},  // rho3 c
+    {5, 2},  // rho4 k
+    {8, 2},  // rho4 (acc + a + c)
+    {6, 3},  // rho5 h
+    {7, 3},  // rho5 (acc + a)
+};
+__global__ void __launch_bounds__(512) k_pghr_rho(int n, const PghrDec* dec, const uint8_t* rho, const uint8_t* status,
+                                                   BA1* mul) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;  // wave-uniform
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  const int pj = PGHR_RHO_MUL[w][0], rj = PGHR_RHO_MUL[w][1];
+  const uint8_t* r = rho + (size_t)64 * i + 16 * rj;  // rho2, rho3, rho4, rho5: 16 LE bytes each
+  uint32_t rw[4];
+  for (int l = 0; l < 4; l++)
+    rw[l] = (uint32_t)r[4 * l] | ((uint32_t)r[4 * l + 1] << 8) | ((uint32_t)r[4 * l + 2] << 16) |
+            ((uint32_t)r[4 * l + 3] << 24);
+  const BA1 q = dec[i].pt[pj];
+  mul[8 * (size_t)i + w] = q.inf ? q : bj1_to_aff(bj1_mul(q, rw, 128));
+}
+
+// lane per proof: the seven G1 operands of the folded check from the products
+//   P1' = -(a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   P7  = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a)          (vk.b, gammaBeta1: comb tables)
+__global__ void __launch_bounds__(64) k_pghr_combine(int n, const PghrDec* dec, const BA1* mul, const uint8_t* rho,
+                                                      const uint32_t* comb, const uint8_t* status, PghrPts* pts) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != ZG_STATUS_OK) return;
+  const PghrDec& d = dec[i];
+  const BA1* m = mul + 8 * (size_t)i;
+  const uint8_t* r = rho + (size_t)64 * i;
+  PghrPts& o = pts[i];
+  o.p[0] = d.pt[0];
+  BJ1 s = bj1_from(d.pt[1]);
+  s = bj1_add_aff(s, m[0]);
+  s = bj1_add_aff(s, m[1]);
+  s = bj1_add_aff(s, m[2]);
+  o.p[1] = ba1_neg(bj1_to_aff(s));
+  o.p[2] = m[3];
+  o.p[3] = m[4];
+  o.p[4] = d.pt[8].inf ? d.pt[8] : ba1_neg(m[5]);
+  o.p[5] = ba1_neg(m[6]);
+  BJ1 t = bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC, r, 16);
+  const BA1 g4 = bj1_to_aff(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 16));
+  t = bj1_add_aff(t, ba1_neg(g4));
+  if (!d.pt[7].inf) t = bj1_add_aff(t, m[7]);
+  o.p[6] = bj1_to_aff(t);
+  o.qb = d.qb;
+}
+
+// the multi-Miller loop of one proof's 7 pairs, split over two waves of a 128-lane block (the same
+// 64 proofs): wave 0 carries pairs 0..3 (fixed G2 points), wave 1 pairs 4, 5 and the proof's own b
+// (its doubling / addition steps), each with its own accumulator (one extra Fq12 squaring per step),
+// so a small batch fills twice the SIMDs (8,192 proofs: 87 -> 49 ms for the whole check). The
+// kernel holds ~460 VGPRs (one wave per SIMD), so from 32,768 proofs -- as many waves as SIMDs --
+// one wave per proof carries all seven pairs (halves 1: the split only adds a squaring per step).
+// fout[halves i + h] = half h's product; k_fe_easy multiplies the two.
+#define ZG_PGHR_SPLIT 4  // pairs [0, SPLIT) on wave 0
+#define ZG_PGHR_SPLIT_BELOW 32768  // batches of fewer proofs run the two-wave split
+__global__ void __launch_bounds__(128) k_pghr_miller(int n, const PghrPts* pts, const BLine* lines,
+                                                      const uint8_t* status, Bq12* fout, int halves) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int h = threadIdx.x >> 6;  // wave-uniform
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
   const PghrPts& P = pts[i];
-  const BA2 qb = P.qb;
-  BH2 t = {qb.x, qb.y, b2_one()};
+  // halves 1 (64-lane blocks): wave 0 alone carries all seven pairs
+  const bool own_b = halves == 1 || h == 1;
+  const int j0 = h ? ZG_PGHR_SPLIT : 0, j1 = (h || halves == 1) ? ZG_BN_FIXED_Q : ZG_PGHR_SPLIT;
+  BA2 qb;
+  BH2 t;
+  if (own_b) {
+    qb = P.qb;
+    t = {qb.x, qb.y, b2_one()};
+  }
   Bq12 f = b12_one();
   int li = 0;
   for (int bit = ZG_BN_ATE_BITS - 2; bit >= -2; bit--) {
@@ -231,11 +296,12 @@ __global__ void __launch_bounds__(64) k_pghr_miller(int n, const PghrPts* pts, c
     const int nsub = bit >= 0 ? (bn_ate_bit(bit) ? 2 : 1) : 1;
     if (bit >= 0) f = b12_sqr(f);
     for (int s = 0; s < nsub; s++, li++) {
-      for (int j = 0; j < ZG_BN_FIXED_Q; j++) {
+      for (int j = j0; j < j1; j++) {
         const BA1 p = P.p[j];
         if (p.inf) continue;
         f = b12_mul_bline(f, lines[(size_t)j * ZG_BN_NLINES + li], p);
       }
+      if (!own_b) continue;
       BLine l;
       if (bit >= 0)
         l = s == 0 ? bh2_dbl_step(&t) : bh2_add_step(&t, qb);
@@ -248,17 +314,18 @@ __global__ void __launch_bounds__(64) k_pghr_miller(int n, const PghrPts* pts, c
       if (!P.p[6].inf) f = b12_mul_bline(f, l, P.p[6]);
     }
   }
-  fout[i] = f;
+  fout[(size_t)halves * i + h] = f;
 }
 
 // the final exponentiation of zg_bn254.h bn_final_exp, split so that no kernel holds more than
 // a few Fq12 values at once (a lane-per-proof Fq12 is 96 VGPRs): the chain's intermediates live in
 // a per-proof HBM workspace w[0..5] = t, b, d, e, g, (spare)
 #define ZG_FE_SLOTS 6
-__global__ void __launch_bounds__(64) k_fe_easy(int n, const Bq12* f, const uint8_t* status, Bq12* w) {
+// halves 2: f holds two partial Miller products per proof (k_pghr_miller), multiplied here
+__global__ void __launch_bounds__(64) k_fe_easy(int n, const Bq12* f, const uint8_t* status, Bq12* w, int halves) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != ZG_STATUS_OK) return;
-  const Bq12 x = f[i];
+  const Bq12 x = halves == 2 ? b12_mul(f[2 * (size_t)i], f[2 * (size_t)i + 1]) : f[i];
   const Bq12 t = b12_mul(b12_conj(x), b12_inv(x));
   w[(size_t)ZG_FE_SLOTS * i + 0] = b12_mul(b12_frob(t, 2), t);
 }
@@ -269,13 +336,15 @@ __global__ void __launch_bounds__(64) k_fe_exp(int n, const uint8_t* status, Bq1
   if (i >= n || status[i] != ZG_STATUS_OK) return;
   Bq12* s = w + (size_t)ZG_FE_SLOTS * i;
   if (STAGE == 1) {
-    const Bq12 b = b12_sqr(b12_exp_by_neg_u(s[0]));
+    const Bq12 b = b12_csqr(b12_exp_by_neg_u(s[0]));  // cyclotomic from here on: Granger-Scott squarings
     s[1] = b;
-    s[2] = b12_mul(b12_sqr(b), b);
+    s[2] = b12_mul(b12_csqr(b), b);
   } else if (STAGE == 2) {
-    s[3] = b12_exp_by_neg_u(s[2]);
+    const Bq12 e = b12_exp_by_neg_u(s[2]);
+    s[3] = e;
+    s[5] = b12_csqr(e);  // stage 3's input (its own kernel holding csqr + the chain spilled ~390 VGPRs)
   } else {
-    s[4] = b12_exp_by_neg_u(b12_sqr(s[3]));
+    s[4] = b12_exp_by_neg_u(s[5]);
   }
 }
 // k = g^-1 e d^-1, l = k b, n = t k e ; result = (t^-1 l)^(p^3) k^(p^2) l^p n == 1 ?
@@ -525,7 +594,11 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   BCHK(alloc((void**)&drho, 64 * n));
   BCHK(alloc((void**)&dst, n));
   BCHK(alloc((void**)&dpts, sizeof(PghrPts) * n));
-  BCHK(alloc((void**)&df, sizeof(Bq12) * n));
+  PghrDec* ddec;
+  BA1* dmul;
+  BCHK(alloc((void**)&ddec, sizeof(PghrDec) * n));
+  BCHK(alloc((void**)&dmul, sizeof(BA1) * 8 * n));
+  BCHK(alloc((void**)&df, sizeof(Bq12) * 2 * n));
   Bq12* dw;
   BCHK(alloc((void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n));
   BCHK(hipMemcpyAsync(dp, proofs, 296 * n, hipMemcpyHostToDevice, st));
@@ -541,12 +614,18 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
     BCHK(hipEventCreate(&e1));
     BCHK(hipEventRecord(e0, st));
   }
-  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, din, dni, drho, d->vk, d->comb,
-                     dpts, dst);
+  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, din, dni, d->vk, d->comb, ddec,
+                     dst);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dpts, d->lines, dst, df);
+  hipLaunchKernelGGL(k_pghr_rho, dim3(bn_blocks(n)), dim3(512), 0, st, (int)n, ddec, drho, dst, dmul);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw);
+  hipLaunchKernelGGL(k_pghr_combine, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
+  BCHK(hipGetLastError());
+  const int halves = n < ZG_PGHR_SPLIT_BELOW ? 2 : 1;
+  hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df,
+                     halves);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw, halves);
   BCHK(hipGetLastError());
   hipLaunchKernelGGL(k_fe_exp<1>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
   BCHK(hipGetLastError());
@@ -584,7 +663,7 @@ int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, u
   const unsigned nb = bn_blocks(n);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_bn_miller1, dim3(nb), dim3(64), 0, st, (int)n, a, b, f);
-    hipLaunchKernelGGL(k_fe_easy, dim3(nb), dim3(64), 0, st, (int)n, f, ok, w);
+    hipLaunchKernelGGL(k_fe_easy, dim3(nb), dim3(64), 0, st, (int)n, f, ok, w, 1);
     hipLaunchKernelGGL(k_fe_exp<1>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);
     hipLaunchKernelGGL(k_fe_exp<2>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);
     hipLaunchKernelGGL(k_fe_exp<3>, dim3(nb), dim3(64), 0, st, (int)n, ok, w);

@@ -7,6 +7,10 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libzg.so")
+# A/B experiments (tooling): ZG_LIB_VARIANT=name loads zebra_amd/libzg_<name>.so, a build of the same
+# sources with other compile-time switches (tools/build_variant.py); never set in production
+if os.environ.get("ZG_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "libzg_%s.so" % os.environ["ZG_LIB_VARIANT"])
 
 KIND_SPEND, KIND_OUTPUT, KIND_SPROUT = 0, 1, 2
 GEN_SPEND_AUTH, GEN_BINDING = 0, 1   # include/zg.h ZG_GEN_*
