@@ -673,6 +673,14 @@ hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const 
                            hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr);          // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
 hipError_t launch_lines_lane(unsigned groups, hipStream_t st, const BatchBufs& b, Fq2* lines, int wpe);  // zg_lines.hip
+// the staged-program kernels of zg_kernels.h, one translation unit each (zg_prog_*.hip)
+hipError_t launch_prog_lines(unsigned groups, hipStream_t st, const BatchBufs& b, Fq2* lines);
+hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines,
+                                   const int* nodes, int m);
+hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
+hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines);
+hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
+                                    int* fail);
 hipError_t launch_jj_comb(hipStream_t st, uint32_t* table);                                    // zg_jubjub.hip
 hipError_t launch_redjubjub(hipStream_t st, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                             const uint8_t* gen, int n, const uint32_t* comb, uint8_t* ok);
@@ -735,26 +743,21 @@ static int run_pipeline(zg_ctx* ctx) {
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
-    hipLaunchKernelGGL(k_lines_fchain, dim3(groups + pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
-                       ctx->d_lines, ctx->d_prog, b.bfail + 1);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
-                       (const Fq2*)ctx->d_lines, (const int*)b.bfail);  // no-op unless bfail / wait failure
+    HIPCHK(launch_prog_lines_fchain(groups + pgroups, ctx->stream, b, ctx->d_lines, ctx->d_prog, b.bfail + 1));
+    // no-op unless bfail / wait failure
+    HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)b.bfail));
   } else {
     const bool lane = ctx->lines_lane > 0 || (ctx->lines_lane < 0 && ctx->npad >= ZG_LINES_LANE_MIN);
     if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
       HIPCHK(launch_lines_lane(groups, ctx->stream, b, ctx->d_lines, ctx->lines_lane == 2 ? 1 : 2));
     } else {                // staged program, lane = proof, wave = product (zg_kernels.h)
-      hipLaunchKernelGGL(k_batch_lines, dim3(groups), dim3(64 * ZG_LINES_NW), 0, ctx->stream, b, ctx->d_lines);
-      HIPCHK(hipGetLastError());
+      HIPCHK(launch_prog_lines(groups, ctx->stream, b, ctx->d_lines));
     }
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     if (quads)
-      hipLaunchKernelGGL(k_batch_fchain4, dim3((unsigned)((ctx->npad / 4 + 63) / 64)), dim3(64 * ZG_FC_NW), 0,
-                         ctx->stream, b, (const Fq2*)ctx->d_lines);
+      HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines));
     else
-      hipLaunchKernelGGL(k_batch_fchain, dim3(pgroups), dim3(64 * ZG_FC_NW), 0, ctx->stream, b,
-                         (const Fq2*)ctx->d_lines, (const int*)nullptr);
+      HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)nullptr));
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
@@ -890,9 +893,7 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
       if (leaves) {  // per-proof Miller leaves exist only on demand (the f-chain writes pair nodes)
         HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
         HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
-        hipLaunchKernelGGL(k_leaf_fchain, dim3(nblocks(m)), dim3(64 * ZG_FC_NW), 0, ctx->side, b,
-                           (const Fq2*)ctx->d_lines, (const int*)ctx->d_nodes, m);
-        HIPCHK(hipGetLastError());
+        HIPCHK(launch_prog_leaf_fchain(nblocks(m), ctx->side, b, (const Fq2*)ctx->d_lines, (const int*)ctx->d_nodes, m));
         HIPCHK(hipEventRecord(ctx->ev[11], ctx->side));
       }
       hipLaunchKernelGGL(k_node_msm, dim3(nblocks((size_t)nb.m * ZG_NKINDS * ZG_MSM_SLOTS * ZG_SHIFTS)),

@@ -20,6 +20,9 @@ namespace zg {
 //   k_batch_fchain: the f-chain (sparse line product, then squaring, fused per step)
 //                   -> ftree leaves
 // A block = 64 proofs; NW waves share each round's independent Fq2 products.
+// The five staged-program kernels are compiled in their own translation units (zg_prog_*.hip,
+// each defines one ZG_TU_PROG_* switch and the launch wrapper zg.hip calls), so the build runs
+// them in parallel: each holds the whole generated operand switch and takes about a minute.
 #define ZG_LINES_NW 4   // one wave per SIMD, 13 LDS slots: two blocks share a CU
 #define ZG_FC_NW 8      // 2 waves per SIMD (256 VGPRs, no spills); msq = 4 rounds
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
@@ -103,10 +106,12 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
     }
   }
 }
+#if defined(ZG_TU_PROG_LINES)
 __global__ void __launch_bounds__(64 * ZG_LINES_NW, 2) k_batch_lines(BatchBufs b, Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_LINES_SLOTS * ZG_ATOM_ROWS * 64];
   lines_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr);
 }
+#endif
 
 // Two proofs per lane: the pair (2j, 2j+1) shares one Miller accumulator, f <- (f l_2j l_2j+1)^2
 // per step, so each step's Fq12 squaring serves both proofs (38 Fq2 products per pair-step
@@ -193,11 +198,13 @@ __device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines
   }
 }
 // gate (optional): {bfail, fused-wait failure}; the launch is a no-op unless one is set
+#if defined(ZG_TU_PROG_FCHAIN)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines, const int* gate) {
   if (gate && gate[0] == 0 && gate[1] == 0) return;
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   fchain_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr, nullptr);
 }
+#endif
 
 // Four proofs per lane (large shards, ZG_QUAD_MIN): the quad (4j .. 4j+3) shares one Miller
 // accumulator, f <- (f l_4j l_4j+1 l_4j+2 l_4j+3)^2 per step (staged programs Q4SQ / Q4: 64 Fq2
@@ -246,10 +253,12 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     reinterpret_cast<Fq2*>(&b.ftree[b.npad / 4 + quad])[wave] = v;
   }
 }
+#if defined(ZG_TU_PROG_FCHAIN4)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, const Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   fchain4_body(b, lines, blockIdx.x, AtomSpace{lds_atoms});
 }
+#endif
 
 // The R-chain and the f-chain as ONE launch for shards whose two grids fit on the device at
 // once (an 8,192-proof rank: 128 lines blocks + 64 f-chain blocks, one block per CU by LDS):
@@ -260,6 +269,7 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, co
 // one off the critical path. Producers never wait; they have the lower block indices and are
 // dispatched first, so the consumers' waits end. proof_active may still see a B that the
 // lines blocks reject (G2 subgroup) as active: bfail then gates the k_batch_fchain re-run.
+#if defined(ZG_TU_PROG_FUSED)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_lines_fchain(BatchBufs b, Fq2* lines, int* prog, int* fail) {
   static_assert(ZG_FCHAIN_SLOTS >= ZG_LINES_SLOTS && ZG_FC_NW >= ZG_LINES_NW, "fused block covers both");
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
@@ -269,11 +279,13 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_lines_fchain(BatchBufs b, Fq2
   else
     fchain_body(b, lines, blockIdx.x - P, AtomSpace{lds_atoms}, prog, fail);
 }
+#endif
 
 // Per-proof Miller leaves ftree[npad + i] for the listed leaf nodes (bisection below a failing
 // pair node; other nodes are skipped), from the line triples the R-chain left in HBM: the
 // single-proof f-chain (staged programs MSQ / M: f = (f l)^2 per step, lane = proof), 1 if the
 // proof is not active. Lanes whose node is not a leaf run on identity lines and store nothing.
+#if defined(ZG_TU_PROG_LINES)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, const Fq2* lines, const int* nodes, int m) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   const AtomSpace at{lds_atoms};
@@ -317,7 +329,9 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, cons
     reinterpret_cast<Fq2*>(&b.ftree[node])[wave] = v;
   }
 }
+#endif
 
+#ifndef ZG_TU_PROG  // the other kernels live in zg.hip's translation unit
 // (single-lane form of the same, kept for reference and tests: pairing's miller_loop of
 // (r_i A_i, B_i) from the affine points)
 __global__ void __launch_bounds__(64) k_leaf_miller(BatchBufs b, const int* nodes, int m) {
@@ -713,5 +727,7 @@ __global__ void __launch_bounds__(256) k_mad_rate(uint64_t* sink, int iters, uin
   }
   if (x == 0x123456789ull) sink[0] = x;
 }
+
+#endif  // ZG_TU_PROG
 
 }  // namespace zg

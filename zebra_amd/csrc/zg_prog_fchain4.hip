@@ -1,0 +1,18 @@
+// zg_prog_fchain4.hip -- translation unit of staged-program kernels of zg_kernels.h (ZG_TU_PROG_FCHAIN4): compiled apart from
+// zg.hip so that the build runs the big generated kernels in parallel; zg.hip launches them through
+// the wrapper below.
+#include <hip/hip_runtime.h>
+
+#include "../../include/zg.h"
+#define ZG_TU_PROG
+#define ZG_TU_PROG_FCHAIN4
+#include "zg_kernels.h"
+
+namespace zg {
+
+hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines) {
+  hipLaunchKernelGGL(k_batch_fchain4, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines);
+  return hipGetLastError();
+}
+
+}  // namespace zg
