@@ -47,7 +47,7 @@ K4_ENTRY_BYTES = 4 + 100
 
 
 def k4_fixed_bytes(npad):
-    c, w, nb, parts = (11, 6, 1024, 4) if npad >= 32768 else (10, 7, 512, 2) if npad >= 8192 else (9, 8, 256, 1)
+    c, w, nb, parts = (11, 6, 1024, 4) if npad >= 32768 else (10, 7, 512, 4) if npad >= 8192 else (9, 8, 256, 2)
     ncount = 3 * w * nb
     return ncount * 4 + (ncount // (64 // parts)) * 2 * 144
 NOMINAL_LANES = 256 * 4 * 16                        # MI355X: CUs x SIMDs x lanes per clock

@@ -135,6 +135,17 @@ static Bq ld_bq(const uint8_t* b) {
   memcpy(x.l, b, 32);
   return bq_to_mont(x);
 }
+// BN254 G2 membership of the twist point with x = (x0, x1) and the chosen square root of the curve
+// equation (32-byte LE canonical coordinates): res[0] = psi(Q) == [6u^2] Q (the product's
+// ba2_in_subgroup), res[1] = [r] Q == O (AffineG2::new); returns 0 if x is not on the twist
+int zgt_bn_g2_membership(const uint8_t* x0, const uint8_t* x1, const uint8_t* y0, const uint8_t* y1, int* res) {
+  const BA2 q = {{ld_bq(x0), ld_bq(x1)}, {ld_bq(y0), ld_bq(y1)}};
+  if (!ba2_on_curve(q)) return 0;
+  res[0] = ba2_in_subgroup(q);
+  res[1] = ba2_in_subgroup_r(q);
+  return 1;
+}
+
 int zgt_bn_g1_decode(const uint8_t* in, uint8_t* out) {
   BA1 p;
   if (!bn_g1_decode(in, &p)) return 0;

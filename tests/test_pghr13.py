@@ -97,3 +97,32 @@ def test_host_bn254_pairing_matches_oracle():
     L.zgt_bn_pairing(g1, g2, out)
     got = [int.from_bytes(out.raw[32 * k:32 * k + 32], "little") for k in range(12)]
     assert got == B.gt_ints(B.final_exponentiation_fc(B.miller_loop([(p, q)])))
+
+
+def test_host_g2_membership_psi_equals_order_check():
+    """the product's G2 membership test psi(Q) == [6u^2] Q (zg_bn254.h ba2_in_subgroup: half the
+    doublings) decides exactly like AffineG2::new's [r] Q == O (ba2_in_subgroup_r, the oracle):
+    G2 points, random twist points, and points of the cofactor subgroup ([r] of a twist point)"""
+    import ctypes
+    import random
+    from oracle import bn254 as BN
+    from tests import hostlib
+    L = hostlib.lib()
+    F = BN._F2
+    rng = random.Random(23)
+    b32 = lambda v: v.to_bytes(32, "little")
+    pts = [(BN.ec_mul(F, BN.G2_GEN, rng.randrange(1, BN.R)), True) for _ in range(3)]
+    while len(pts) < 9:
+        x = (rng.randrange(BN.P), rng.randrange(BN.P))
+        y = BN.f2_sqrt(F.add(F.mul(F.mul(x, x), x), F.b))
+        if y is None:
+            continue
+        pts.append(((x, y), False))
+        if len(pts) % 3 == 0:
+            c = BN.ec_mul(F, (x, y), BN.R)   # order divides the cofactor 2p - r
+            if c is not None:
+                pts.append((c, False))
+    for (x, y), want in pts:
+        res = (ctypes.c_int * 2)()
+        assert L.zgt_bn_g2_membership(b32(x[0]), b32(x[1]), b32(y[0]), b32(y[1]), res) == 1
+        assert res[0] == res[1] == int(want)

@@ -163,26 +163,31 @@ ZG_INL Bq2 b2_pow(const Bq2& a, const uint32_t* e, int nbits) {
   }
   return r;
 }
-// a square root (eprint 2012/685 algorithm 9, p = 3 mod 4), false for a non-residue
+// a square root in Fq2 = Fq[u]/(u^2 + 1) by the norm ("complex") method, false for a non-residue:
+// s = sqrt(a0^2 + a1^2); x = t^((p+1)/4) for t = (a0 + s)/2 -- if x^2 == t the root is
+// (x, a1 / 2x), else x^2 == -t (p = 3 mod 4) and (a0 - s)/2 = -a1^2 / 4t is the square of a1 / 2x,
+// the root (a1 / 2x, x). Two Fq exponentiations and one inversion, against two Fq2 exponentiations
+// of eprint 2012/685 algorithm 9 (round 2's form): any root serves, bn_g2_decode picks y or -y by the
+// encoding's flag afterwards.
 ZG_INL bool b2_sqrt(const Bq2& a, Bq2* r) {
-  if (b2_is_zero(a)) {
-    *r = a;
-    return true;
+  if (bq_is_zero(a.c1)) {  // a in Fq: sqrt(a0), or sqrt(-a0) u (-1 is a non-residue)
+    Bq s;
+    if (bq_sqrt(a.c0, &s)) {
+      *r = {s, bq_zero()};
+      return true;
+    }
+    const bool ok = bq_sqrt(bq_neg(a.c0), &s);
+    *r = {bq_zero(), s};
+    return ok;
   }
-  const Bq2 a1 = b2_pow(a, BQ_EXP_SQRT2, 254);
-  const Bq2 alpha = b2_mul(b2_sqr(a1), a);
-  const Bq2 a0 = b2_mul(b2_conj(alpha), alpha);
-  const Bq2 m1 = {bq_neg(bq_one()), bq_zero()};
-  if (b2_eq(a0, m1)) return false;
-  const Bq2 x0 = b2_mul(a1, a);
-  Bq2 s;
-  if (b2_eq(alpha, m1)) {
-    s = {bq_neg(x0.c1), x0.c0};  // x0 u
-  } else {
-    s = b2_mul(b2_pow(b2_add(alpha, b2_one()), BQ_EXP_HALF, 253), x0);
-  }
-  *r = s;
-  return b2_eq(b2_sqr(s), a);
+  Bq s;
+  if (!bq_sqrt(bq_add(bq_sqr(a.c0), bq_sqr(a.c1)), &s)) return false;
+  Bq t = bq_add(a.c0, s);
+  t = bq_mul(t, bq_c(BQ_HALF));  // (a0 + s) / 2 != 0 since a1 != 0
+  const Bq x = bq_pow(t, BQ_EXP_SQRT, 254);
+  const Bq w = bq_mul(a.c1, bq_inv(bq_dbl(x)));
+  *r = bq_eq(bq_sqr(x), t) ? Bq2{x, w} : Bq2{w, x};
+  return b2_eq(b2_sqr(*r), a);
 }
 
 // ---- Fq6
@@ -360,6 +365,21 @@ ZG_INL BJ1 bj1_add_aff(const BJ1& p, const BA1& q) {
   const Bq Z3 = bq_sub(bq_sub(bq_sqr(bq_add(p.Z, H)), Z1Z1), HH);
   return {X3, Y3, Z3};
 }
+// p + q, both Jacobian (add-2007-bl with the special cases)
+ZG_INL BJ1 bj1_add(const BJ1& p, const BJ1& q) {
+  if (bj1_is_inf(p)) return q;
+  if (bj1_is_inf(q)) return p;
+  const Bq Z1Z1 = bq_sqr(p.Z), Z2Z2 = bq_sqr(q.Z);
+  const Bq U1 = bq_mul(p.X, Z2Z2), U2 = bq_mul(q.X, Z1Z1);
+  const Bq S1 = bq_mul(bq_mul(p.Y, q.Z), Z2Z2), S2 = bq_mul(bq_mul(q.Y, p.Z), Z1Z1);
+  const Bq H = bq_sub(U2, U1), rr = bq_dbl(bq_sub(S2, S1));
+  if (bq_is_zero(H)) return bq_is_zero(rr) ? bj1_dbl(p) : bj1_inf();
+  const Bq I = bq_sqr(bq_dbl(H)), J = bq_mul(H, I), V = bq_mul(U1, I);
+  const Bq X3 = bq_sub(bq_sub(bq_sqr(rr), J), bq_dbl(V));
+  const Bq Y3 = bq_sub(bq_mul(rr, bq_sub(V, X3)), bq_dbl(bq_mul(S1, J)));
+  const Bq Z3 = bq_mul(bq_sub(bq_sub(bq_sqr(bq_add(p.Z, q.Z)), Z1Z1), Z2Z2), H);
+  return {X3, Y3, Z3};
+}
 ZG_INL BA1 bj1_to_aff(const BJ1& p) {
   if (bj1_is_inf(p)) return {bq_zero(), bq_zero(), true};
   const Bq zi = bq_inv(p.Z), zi2 = bq_sqr(zi);
@@ -404,8 +424,9 @@ ZG_INL BJ2 bj2_add_aff(const BJ2& p, const BA2& q) {
   const Bq2 Z3 = b2_sub(b2_sub(b2_sqr(b2_add(p.Z, H)), Z1Z1), HH);
   return {X3, Y3, Z3};
 }
-// AffineG2::new's order check: [r] Q == O
-ZG_INL bool ba2_in_subgroup(const BA2& q) {
+// AffineG2::new's order check, [r] Q == O, as the bn crate runs it (kept for tests; the product
+// uses ba2_in_subgroup below)
+ZG_INL bool ba2_in_subgroup_r(const BA2& q) {
   BJ2 acc = {b2_one(), b2_one(), b2_zero()};
   for (int i = 253; i >= 0; i--) {
     acc = bj2_dbl(acc);
@@ -472,6 +493,24 @@ ZG_INL BA2 ba2_frob(const BA2& q) {
   return {b2_mul(b2_conj(q.x), b2_c(BQ_FROB1_2)), b2_mul(b2_conj(q.y), b2_c(BQ_FROB1_3))};
 }
 ZG_INL BA2 ba2_frob2(const BA2& q) { return {b2_mul(q.x, b2_c(BQ_FROB2_2)), b2_mul(q.y, b2_c(BQ_FROB2_3))}; }
+
+// G2 membership decided as psi(Q) == [6u^2] Q (a 127-bit scalar: half the doublings of [r] Q).
+// psi (untwist-Frobenius-twist, ba2_frob) satisfies psi^2 - t psi + p = 0 on E'(Fq2) and acts on G2
+// as [p] = [p mod r] = [6u^2]. The endomorphism psi - [6u^2] has degree (6u^2)^2 - t 6u^2 + p =
+// p - 6u^2 = r (t = 6u^2 + 1), so its kernel is exactly G2: for Q on the twist,
+// psi(Q) = [6u^2] Q  <=>  [r] Q = O (AffineG2::new). tests/test_pghr13.py compares the two.
+ZG_INL bool ba2_in_subgroup(const BA2& q) {
+  static constexpr uint32_t SIX_U2[4] = {0xe87cfd46u, 0xf83e9682u, 0xeeb859fbu, 0x6f4d8248u};  // 6u^2
+  BJ2 acc = {q.x, q.y, b2_one()};
+  for (int i = 125; i >= 0; i--) {  // bit 126 is the leading one
+    acc = bj2_dbl(acc);
+    if ((SIX_U2[i >> 5] >> (i & 31)) & 1u) acc = bj2_add_aff(acc, q);
+  }
+  if (b2_is_zero(acc.Z)) return false;  // [6u^2] Q = O while psi(Q) is finite
+  const BA2 s = ba2_frob(q);
+  const Bq2 z2 = b2_sqr(acc.Z);
+  return b2_eq(acc.X, b2_mul(s.x, z2)) && b2_eq(acc.Y, b2_mul(s.y, b2_mul(z2, acc.Z)));
+}
 
 #define ZG_BN_ATE_BITS 65  // 6u + 2
 ZG_INL bool bn_ate_bit(int i) { return (BN_ATE[i >> 5] >> (i & 31)) & 1u; }

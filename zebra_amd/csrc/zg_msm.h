@@ -46,7 +46,9 @@ namespace zg {
                                                    // r03: 4,096 gave 16 blocks and a 5.3 ms launch)
 
 // the window shape of a batch of npad (padded) proofs: c bits, w windows, nb = 2^(c-1) buckets
-// per (key, window), parts = lanes per bucket in the bucket phase
+// per (key, window), parts = lanes per bucket in the bucket phase (small shards: more parts, so a
+// lane's chain of dependent additions -- its share of the bucket, then the wave's LDS levels -- is
+// shorter; the bucket phase is latency-bound there)
 #define ZG_MSM_BITS 66
 struct MsmShape {
   int c, w, nb, parts;
@@ -60,8 +62,8 @@ struct MsmShape {
 };
 ZG_HD inline MsmShape msm_shape(size_t npad) {
   if (npad >= 32768) return {11, 6, 1024, 4};
-  if (npad >= 8192) return {10, 7, 512, 2};
-  return {9, 8, 256, 1};
+  if (npad >= 8192) return {10, 7, 512, 4};
+  return {9, 8, 256, 2};
 }
 
 // window w of the 66-bit scalar lo + 2^64 hi (S.width(w) bits from bit S.shift(w)), as a signed

@@ -181,7 +181,9 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
   __syncthreads();
   sh[s] = x;
   __syncthreads();
-  for (int d = 32; d >= 1; d >>= 1) {
+  int top = 1;
+  while (top < ns) top <<= 1;
+  for (int d = top / 2; d >= 1; d >>= 1) {  // the lanes past ns hold infinity
     G1J u = sh[s];
     if (s < d) u = jac_add_full(u, sh[s + d]);
     __syncthreads();

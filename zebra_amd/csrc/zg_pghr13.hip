@@ -151,18 +151,54 @@ struct PghrDec {
   BA2 qb;
 };
 
-// lane per proof: Proof::from_raw's decodes and checks, acc = ic0 + sum x_j ic_{j+1} (combs)
-__global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* proofs, const uint8_t* inputs,
-                                                   const uint8_t* ninputs, const BnVK* vk, const uint32_t* comb,
+// Proof::from_raw's point decodes: the seven G1 points one per wave of a 448-lane block (64 proofs;
+// bytes a 0, a' 33, b' 131, c 164, c' 197, k 230, h 263) and the G2 point b (bytes 66..130: the
+// Fq2 square root and the G2 membership test, far heavier) in a launch of its own, lane per proof,
+// so the light waves do not hold a block open behind it -> dec, verdicts -> okb[8 i + w] (w = 2: b).
+__device__ __constant__ const int16_t PGHR_DEC_OFF[7] = {0, 33, 131, 164, 197, 230, 263};
+__device__ __constant__ const int8_t PGHR_DEC_OK[7] = {0, 1, 3, 4, 5, 6, 7};
+__global__ void __launch_bounds__(448) k_pghr_decode_g1(int n, const uint8_t* proofs, PghrDec* dec, uint8_t* okb) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;  // wave-uniform: slot w of dec.pt
+  if (i >= n) return;
+  BA1 a;
+  const bool ok = bn_g1_decode(proofs + (size_t)296 * i + PGHR_DEC_OFF[w], &a);
+  if (ok) dec[i].pt[w] = a;
+  okb[8 * (size_t)i + PGHR_DEC_OK[w]] = ok;
+}
+__global__ void __launch_bounds__(64) k_pghr_decode_g2(int n, const uint8_t* proofs, PghrDec* dec, uint8_t* okb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  BA2 q;
+  const bool ok = bn_g2_decode(proofs + (size_t)296 * i + 66, &q);
+  if (ok) dec[i].qb = q;
+  okb[8 * (size_t)i + 2] = ok;
+}
+
+// x_j ic_{j+1} for the nine input slots, one per wave of a 576-lane block (byte-window combs, 32
+// mixed additions each) -> accp[9 i + j] (infinity past the proof's input count); canonicity is
+// k_pghr_prep's
+__global__ void __launch_bounds__(576) k_pghr_accp(int n, const uint8_t* inputs, const uint8_t* ninputs,
+                                                    const BnVK* vk, const uint32_t* comb, BJ1* accp) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = threadIdx.x >> 6;  // wave-uniform
+  if (i >= n) return;
+  int cnt = ninputs ? ninputs[i] : 9;
+  cnt = cnt < vk->ic_len - 1 ? cnt : vk->ic_len - 1;
+  BJ1 r = bj1_inf();
+  if (j < cnt) r = bn_comb_mul(r, comb, j + 1, inputs + (size_t)9 * 32 * i + 32 * j, 32);
+  accp[9 * (size_t)i + j] = r;
+}
+
+// lane per proof: the statuses in the reference's order (a failed decode, then a non-canonical
+// input), acc = ic0 + the nine comb products, acc + a and acc + a + c
+__global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* inputs, const uint8_t* ninputs,
+                                                   const BnVK* vk, const uint8_t* okb, const BJ1* accp,
                                                    PghrDec* dec, uint8_t* status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint8_t* pr = proofs + (size_t)296 * i;
-  BA1 a, ap, bp, c, cp, k, h;
-  BA2 qb;
-  const bool ok = bn_g1_decode(pr, &a) && bn_g1_decode(pr + 33, &ap) && bn_g2_decode(pr + 66, &qb) &&
-                  bn_g1_decode(pr + 131, &bp) && bn_g1_decode(pr + 164, &c) && bn_g1_decode(pr + 197, &cp) &&
-                  bn_g1_decode(pr + 230, &k) && bn_g1_decode(pr + 263, &h);
+  bool ok = true;
+  for (int w = 0; w < 8; w++) ok = ok && okb[8 * (size_t)i + w];
   if (!ok) {
     status[i] = ZG_STATUS_DECODE_INVALID;
     return;
@@ -177,34 +213,23 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* proofs, 
     for (int l = 0; l < 8; l++)
       x.l[l] = (uint32_t)xin[32 * j + 4 * l] | ((uint32_t)xin[32 * j + 4 * l + 1] << 8) |
                ((uint32_t)xin[32 * j + 4 * l + 2] << 16) | ((uint32_t)xin[32 * j + 4 * l + 3] << 24);
-    bool lt_r = false;  // x < r (bn::Fr)
-    {
-      uint64_t br = 0;
-      for (int l = 0; l < 8; l++) {
-        const uint64_t d = (uint64_t)x.l[l] - BN_R[l] - br;
-        br = (d >> 63) & 1u;
-      }
-      lt_r = br != 0;
+    uint64_t br = 0;  // x < r (bn::Fr)
+    for (int l = 0; l < 8; l++) {
+      const uint64_t d = (uint64_t)x.l[l] - BN_R[l] - br;
+      br = (d >> 63) & 1u;
     }
-    if (!lt_r) {
+    if (!br) {
       status[i] = ZG_STATUS_INPUT_NONCANONICAL;
       return;
     }
-    acc = bn_comb_mul(acc, comb, j + 1, xin + 32 * j, 32);
+    acc = bj1_add(acc, accp[9 * (size_t)i + j]);
   }
+  PghrDec& o = dec[i];
+  const BA1 a = o.pt[0], c = o.pt[3];
   const BA1 acca = bj1_to_aff(acc);
   const BA1 aa = ba1_add(acca, a);  // acc + a
-  PghrDec& o = dec[i];
-  o.pt[0] = a;
-  o.pt[1] = ap;
-  o.pt[2] = bp;
-  o.pt[3] = c;
-  o.pt[4] = cp;
-  o.pt[5] = k;
-  o.pt[6] = h;
   o.pt[7] = aa;
   o.pt[8] = ba1_add(aa, c);  // acc + a + c
-  o.qb = qb;
   status[i] = ZG_STATUS_OK;
 }
 
@@ -596,8 +621,12 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   BCHK(alloc((void**)&dpts, sizeof(PghrPts) * n));
   PghrDec* ddec;
   BA1* dmul;
+  BJ1* daccp;
+  uint8_t* dokb;
   BCHK(alloc((void**)&ddec, sizeof(PghrDec) * n));
   BCHK(alloc((void**)&dmul, sizeof(BA1) * 8 * n));
+  BCHK(alloc((void**)&daccp, sizeof(BJ1) * 9 * n));
+  BCHK(alloc((void**)&dokb, 8 * n));
   BCHK(alloc((void**)&df, sizeof(Bq12) * 2 * n));
   Bq12* dw;
   BCHK(alloc((void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n));
@@ -614,7 +643,13 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
     BCHK(hipEventCreate(&e1));
     BCHK(hipEventRecord(e0, st));
   }
-  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, din, dni, d->vk, d->comb, ddec,
+  hipLaunchKernelGGL(k_pghr_decode_g1, dim3(bn_blocks(n)), dim3(448), 0, st, (int)n, dp, ddec, dokb);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_pghr_decode_g2, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, ddec, dokb);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_pghr_accp, dim3(bn_blocks(n)), dim3(576), 0, st, (int)n, din, dni, d->vk, d->comb, daccp);
+  BCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, din, dni, d->vk, dokb, daccp, ddec,
                      dst);
   BCHK(hipGetLastError());
   hipLaunchKernelGGL(k_pghr_rho, dim3(bn_blocks(n)), dim3(512), 0, st, (int)n, ddec, drho, dst, dmul);
