@@ -267,6 +267,9 @@ def main():
     os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch
     import torch.distributed as dist
+    if use_dist and "RANK" not in os.environ:  # --dist outside torch.distributed.run: a world of one
+        os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                           "MASTER_PORT": os.environ.get("MASTER_PORT", str(29500 + os.getpid() % 1000))})
     if use_dist:
         # RCCL prints its version banner on stdout while it initialises: keep stdout for the one
         # JSON line (fd-level, the banner comes from C)
