@@ -27,6 +27,8 @@ void zgt_g1_check_glv(const uint8_t* x, const uint8_t* y, uint64_t a, uint64_t b
   res[1] = g1_in_subgroup_d(p);
   const G1A w = jac_to_aff(g1_glv_mul(p, a, b));
   const G1A d = jac_to_aff(g1_glv_mul_d(p, a, b));
+  const G1A d2 = jac_to_aff(g1_glv_mul_w2(p, a, b));
+  res[2] = d2.inf == d.inf && (d.inf || (fq_eq(d2.x, d.x) && fq_eq(d2.y, d.y)));
   memset(out_w, 0, 96);
   memset(out_d, 0, 96);
   if (!w.inf) {

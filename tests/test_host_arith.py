@@ -269,7 +269,8 @@ def _g1_points(rng, n):
 
 
 def test_g1_digit_arith_equals_word_form():
-    """the decode kernels' lazy-digit G1 arithmetic (zg_fqd.h: g1_in_subgroup_d, g1_glv_mul_d)
+    """the decode kernels' lazy-digit G1 arithmetic (zg_fqd.h: g1_in_subgroup_d, g1_glv_mul_d and the
+    two-column g1_glv_mul_w2)
     against the word form (zg_curve.h / zg_groth16.h) and the oracle: subgroup verdicts on G1
     points, curve points outside G1 and the order-3 points (0, +-2) (exceptional additions in the
     chain), and r A for random and extreme GLV scalars"""
@@ -282,10 +283,11 @@ def test_g1_digit_arith_equals_word_form():
     for (x, y), ing1 in _g1_points(rng, 6):
         for a, b in [(rng.getrandbits(64), rng.getrandbits(64)), (0, 0), ((1 << 64) - 1, (1 << 64) - 1),
                      ((1 << 64) - 1, 0), (0, (1 << 64) - 1)]:
-            res = (ctypes.c_int * 2)()
+            res = (ctypes.c_int * 3)()
             ow, od = ctypes.create_string_buffer(96), ctypes.create_string_buffer(96)
             L.zgt_g1_check_glv(fq_b(x), fq_b(y), a, b, res, ow, od)
             assert res[0] == res[1] == int(ing1)
             assert ow.raw == od.raw
+            assert res[2] == 1 or not ing1   # the two-column GLV (decode's) agrees on G1 points
             if ing1 and a == 0 and b == 0:   # k = 1: r A = A
                 assert ow.raw == fq_b(x) + fq_b(y)

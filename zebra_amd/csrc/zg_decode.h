@@ -14,7 +14,7 @@ namespace zg {
 #endif
 #if ZG_DECODE_FQD
 #define ZG_DEC_SUBGROUP g1_in_subgroup_d
-#define ZG_DEC_GLV g1_glv_mul_d
+#define ZG_DEC_GLV g1_glv_mul_w2  // two columns per step (g1_glv_mul_d: one)
 #else
 #define ZG_DEC_SUBGROUP g1_in_subgroup
 #define ZG_DEC_GLV g1_glv_mul

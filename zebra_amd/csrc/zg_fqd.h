@@ -240,7 +240,7 @@ ZG_INL G1D g1d_dbl(const G1D& p) {
   return {X3, Y3, Z3};
 }
 
-// madd-2007-bl with complete case handling: p + q for q affine and finite, qx < 2p, qy < 3p.
+// madd-2007-bl with complete case handling: p + q for q affine and finite, qx < 2p, qy < 4p.
 // In: the invariant. Out: X < 9p, Y < 7p, Z < 4p (or g1d_dbl's, or q itself). 11 products.
 ZG_INL G1D g1d_add_aff(const G1D& p, const FqD& qx, const FqD& qy) {
   if (g1d_is_inf(p)) return g1d_from_aff(qx, qy);

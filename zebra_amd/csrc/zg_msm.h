@@ -24,8 +24,9 @@
 //                  then the wave forms its segment's T = sum_j (j + 1) S_j and U = sum_j S_j by
 //                  an LDS suffix scan and an LDS tree (wavefront-level, no atomics on points)
 //   k_msm_group    a wave per (key, window): sum_s (T_s + 64/P s U_s) over the group's segments
-//                  (suffix scan of U, doublings by 64/P, tree) -> the window sum
-//   k_msm_final    per key: sum_w 2^shift(w) W_w (Horner) -> the C-sum root node ctree[1]
+//                  (suffix scan of U, doublings by 64/P, tree) -> the window sum, already scaled by
+//                  2^shift(w) (the windows' doubling chains run in parallel, one per group)
+//   k_msm_final    per key: sum_w of the scaled window sums -> the C-sum root node ctree[1]
 //   k_fr_root / k_fr_final  the root Fr sums S_k0 = sum r_i, S_kj = sum r_i x_ij per key
 // The random batch scalars are secret and uniform, so bucket sizes are Poisson whatever the
 // proofs: ~2N/2^(c-1) entries per bucket and key. Per-proof r_i C_i (GLV) and the full C / Fr
@@ -42,7 +43,7 @@ namespace zg {
 #define ZG_MSM_SEG_MAX 64                          // segments (waves) per (key, window)
 #define ZG_MSM_BT 256                              // threads per k_msm_bucket block (4 waves)
 #define ZG_MSM_SCAN_T 1024                         // lanes of the scan block
-#define ZG_FR_CHUNK 256                            // proofs per k_fr_root block (256 blocks at 64k;
+#define ZG_FR_CHUNK 64                             // proofs per k_fr_root block (1,024 blocks at 64k;
                                                    // r03: 4,096 gave 16 blocks and a 5.3 ms launch)
 
 // the window shape of a batch of npad (padded) proofs: c bits, w windows, nb = 2^(c-1) buckets

@@ -190,20 +190,22 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
     sh[s] = u;
     __syncthreads();
   }
-  if (s == 0) m.wsum[g] = sh[0];
+  if (s == 0) {  // 2^shift(w) W_w: this window's part of sum_w 2^shift(w) W_w
+    G1J x = sh[0];
+    const int w = g % S.w;
+    for (int q = 0; q < S.shift(w); q++) x = jac_dbl_inl(x);
+    m.wsum[g] = x;
+  }
 }
 
-// per key: sum_w 2^shift(w) W_w -> the root node of the C-sum tree (node 1)
+// per key: sum_w of the scaled window sums (k_msm_group) -> the root node of the C-sum tree (node 1)
 __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
   const int kind = threadIdx.x;
   if (kind >= ZG_NKINDS) return;
   const MsmShape S = m.s;
-  G1J acc = m.wsum[kind * S.w + S.w - 1];
-  for (int w = S.w - 2; w >= 0; w--) {
-    for (int q = 0; q < S.width(w); q++) acc = jac_dbl_inl(acc);  // 2^(shift(w + 1) - shift(w))
-    acc = jac_add_full(acc, m.wsum[kind * S.w + w]);
-  }
+  G1J acc = m.wsum[kind * S.w];
+  for (int w = 1; w < S.w; w++) acc = jac_add_full(acc, m.wsum[kind * S.w + w]);
   b.ctree[1 * ZG_NKINDS + kind] = acc;
 }
 
@@ -219,6 +221,7 @@ __global__ void __launch_bounds__(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G) k_fr_root(Bat
   const int chunk = blockIdx.x, t = threadIdx.x, ks = t % KS, g = t / KS;
   Fr acc = fp_zero<FrM>();
   const int lo = chunk * ZG_FR_CHUNK, hi = min(lo + ZG_FR_CHUNK, b.npad);
+#pragma unroll 4
   for (int i = lo + g; i < hi; i += ZG_FR_G) acc = fr_add(acc, b.stree[(size_t)(b.npad + i) * KS + ks]);
   sh[t] = acc;
   __syncthreads();
