@@ -40,7 +40,7 @@ for s in $STEPS; do
   prof)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 9 --warmup 0 > $O/prof_bench.json 2> $O/prof_bench.err || { echo "rocprof failed"; tail -30 $O/prof_bench.err; exit 1; }
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof_bench_iso.json 2> $O/prof_bench_iso.err || { echo "rocprof iso failed"; tail -30 $O/prof_bench_iso.err; exit 1; }
+    ZG_SERIAL_SIDE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_iso -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 6 --warmup 0 --inflight 1 --sync-verdict > $O/prof_bench_iso.json 2> $O/prof_bench_iso.err || { echo "rocprof iso failed"; tail -30 $O/prof_bench_iso.err; exit 1; }
     cd $R && for k in prof prof_iso; do python3 tools/rocpd_stats.py $O/$k/run_results.db $O/kernel_stats_${k#prof}.csv; done ;;
   variants)
     for v in $VARIANTS; do

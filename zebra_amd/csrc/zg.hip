@@ -145,7 +145,8 @@ struct zg_ctx {
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
   int lines_lane = -1;      // ZG_LINES_LANE: -1 auto (the straight-line R-chain from ZG_LINES_LANE_MIN padded
-                            // proofs, else the staged program), 1 / 2 always straight-line sized for 2 / 1
+                            // proofs, sized for 1 wave per SIMD when the batch is alone on the device, else
+                            // 2; the staged program below), 1 / 2 always straight-line sized for 2 / 1
                             // waves per SIMD, 0 always the staged program (zg_kernels.h)
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
@@ -749,7 +750,12 @@ static int run_pipeline(zg_ctx* ctx) {
   } else {
     const bool lane = ctx->lines_lane > 0 || (ctx->lines_lane < 0 && ctx->npad >= ZG_LINES_LANE_MIN);
     if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
-      HIPCHK(launch_lines_lane(groups, ctx->stream, b, ctx->d_lines, ctx->lines_lane == 2 ? 1 : 2));
+      // register budget: auto sizes for one wave per SIMD (512 VGPRs: 64k alone 3.70 -> 3.38 ms) when no
+      // other batch is on the device, else two (in flight the SIMDs' second slot serves the other
+      // batches' kernels: 4 in flight 14.93 vs 14.47 ms per batch; profiles/r03c_bench_lines_lane*.json)
+      const bool alone = ctx->dev->inflight.load(std::memory_order_relaxed) == 0;
+      const int wpe = ctx->lines_lane == 2 ? 1 : ctx->lines_lane == 1 ? 2 : alone ? 1 : 2;
+      HIPCHK(launch_lines_lane(groups, ctx->stream, b, ctx->d_lines, wpe));
     } else {                // staged program, lane = proof, wave = product (zg_kernels.h)
       HIPCHK(launch_prog_lines(groups, ctx->stream, b, ctx->d_lines));
     }
