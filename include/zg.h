@@ -291,8 +291,8 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
  * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
  * (k_batch_fchain4; shards of 8,192 or more padded proofs -- ZG_QUAD_MIN -- or as ZG_FCHAIN_QUADS
- * forces). Writes min(n, 8) values,
- * zero beyond. */
+ * forces), [8] zg_pghr13_verify calls with proofs, [9] those whose one batch check failed (the
+ * call then ran the per-proof check for the exact statuses). Writes min(n, 10) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

@@ -131,3 +131,31 @@ def test_gpu_pghr13_keys_per_context():
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_batch_check_paths(ctx):
+    """the one-check-per-call path (zg_pghr13.hip: the key pairs on the batch's sums, one single-pair
+    loop per proof, one final exponentiation): 2,048 valid proofs, then the same with decode-invalid
+    and non-canonical cases mixed in (excluded from the batch, which still passes), then with one
+    VERIFY_FAILED proof (the batch fails and the per-proof path gives the exact statuses)"""
+    from zebra_amd import zg
+    cases = GOLDEN["cases"]
+    valid = [c for c in cases if c["status"] == zg.STATUS_OK]
+    skipped = [c for c in cases if c["status"] not in (zg.STATUS_OK, zg.STATUS_VERIFY_FAILED)]
+    failing = [c for c in cases if c["status"] == zg.STATUS_VERIFY_FAILED]
+    assert valid and skipped and failing
+    rnd = random.Random(9)
+    base = [valid[rnd.randrange(len(valid))] for _ in range(2048)]
+    for extra, fails in (([], 0), (skipped, 0), (skipped + failing[:1], 1)):
+        batch = list(base)
+        for c in extra:
+            batch[rnd.randrange(len(batch))] = c
+        st0 = ctx.stats()
+        got = ctx.pghr13_verify([bytes.fromhex(c["proof"]) for c in batch], [_inputs(c) for c in batch])
+        assert got == [c["status"] for c in batch]
+        st1 = ctx.stats()
+        assert st1["pghr13_calls"] == st0["pghr13_calls"] + 1
+        # the batch check alone decides an all-valid call (a wrong batch check would only show here:
+        # the per-proof path would still give the right statuses)
+        assert st1["pghr13_batch_failures"] - st0["pghr13_batch_failures"] == fails

@@ -28,7 +28,7 @@ using namespace zg;
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 13
 #define ZG_NTIMINGS 9
-#define ZG_NSTATS 8
+#define ZG_NSTATS 10
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
 #define ZG_LINES_LANE_MIN 32768  // straight-line R-chain from here (r03: 64k 14.93 -> 14.47 ms per batch in
@@ -55,7 +55,7 @@ void bn_dev_free(BnDev* d);
 int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, const BnKey** out, std::string* err);
 int bn_pghr13_verify(const BnKey* k, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
                      const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
-                     std::string* err);
+                     bool* batch_failed, std::string* err);
 int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt, std::string* err);
 }  // namespace zg
 
@@ -1561,25 +1561,39 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
   }
   HIPCHK(hipSetDevice(ctx->device));
   if (!n) return ZG_OK;
-  // the equality weights rho_2..rho_5 (16 bytes each): seeded contexts (tests) derive them,
-  // others take them from the OS
-  std::vector<uint8_t> rho(64 * n);
+  // the equality weights rho_2..rho_5 and rho_1 (16 bytes each, zg_pghr13.hip ZG_PGHR_RHO_BYTES):
+  // seeded contexts (tests) derive them, others take them from the OS
+  std::vector<uint8_t> rho(80 * n);
   if (ctx->seeded) {
     for (size_t i = 0; i < n; i++) {
+      uint8_t le[8], h1[64];
       Blake2b h(64);
       h.update("zg-pghr13-rho", 13);
-      uint8_t le[8];
       for (int b = 0; b < 8; b++) le[b] = (uint8_t)(ctx->seed >> (8 * b));
       h.update(le, 8);
       for (int b = 0; b < 8; b++) le[b] = (uint8_t)((uint64_t)i >> (8 * b));
       h.update(le, 8);
-      h.final(&rho[64 * i]);
+      h.final(&rho[80 * i]);
+      Blake2b g(64);
+      g.update("zg-pghr13-rho1", 14);
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)(ctx->seed >> (8 * b));
+      g.update(le, 8);
+      for (int b = 0; b < 8; b++) le[b] = (uint8_t)((uint64_t)i >> (8 * b));
+      g.update(le, 8);
+      g.final(h1);
+      memcpy(&rho[80 * i + 64], h1, 16);
     }
   } else if (!os_random(rho.data(), rho.size())) {
     return fail(ctx, ZG_E_INVAL, "getrandom failed");
   }
-  return bn_pghr13_verify(ctx->bn_key, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status, kernel_ms,
-                          &ctx->err);
+  bool batch_failed = false;
+  const int rc = bn_pghr13_verify(ctx->bn_key, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status,
+                                  kernel_ms, &batch_failed, &ctx->err);
+  if (rc == ZG_OK && n) {
+    ctx->stats[8]++;
+    if (batch_failed) ctx->stats[9]++;
+  }
+  return rc;
 }
 
 extern "C" int zg_bn254_pairing(zg_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt) {

@@ -6,7 +6,8 @@
 // are folded into one product with random 128-bit weights rho_2..rho_5 (rho_1 = 1):
 //
 //   e(a, A) e(P1', P2) e(rho3 c, C) e(rho4 k, G) e(P5, GB2) e(P6, Z) e(P7, b) == 1
-//   P1' = -(a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   P1' = -(rho1 a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   (and P0 = rho1 a: with rho1 random too, one proof's check and the batch's share its operands)
 //   P7  = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a)
 //
 // which holds for all rho iff each equality holds (a false proof passes with probability
@@ -25,6 +26,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -236,7 +238,9 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* inputs, 
 // the eight 128-bit products rho_j Q of a proof, one per wave of a 512-lane block (64 proofs):
 // wave w computes PGHR_RHO_MUL[w] = (point, rho index), affine, -> mul[8 i + w]. One lane per
 // proof ran them back to back (eight 128-bit double-and-add chains at one wave per SIMD).
-__device__ __constant__ const int8_t PGHR_RHO_MUL[8][2] = {
+#define ZG_PGHR_RHO_BYTES 80  // rho2, rho3, rho4, rho5, rho1: 16 LE bytes each
+#define ZG_PGHR_NMUL 10
+__device__ __constant__ const int8_t PGHR_RHO_MUL[ZG_PGHR_NMUL][2] = {
     {2, 0},  // rho2 b'
     {4, 1},  // rho3 c'
     {3, 3},  // rho5 c
@@ -245,35 +249,38 @@ __device__ __constant__ const int8_t PGHR_RHO_MUL[8][2] = {
     {8, 2},  // rho4 (acc + a + c)
     {6, 3},  // rho5 h
     {7, 3},  // rho5 (acc + a)
+    {0, 4},  // rho1 a
+    {1, 4},  // rho1 a'
 };
-__global__ void __launch_bounds__(512) k_pghr_rho(int n, const PghrDec* dec, const uint8_t* rho, const uint8_t* status,
-                                                   BA1* mul) {
+__global__ void __launch_bounds__(64 * ZG_PGHR_NMUL) k_pghr_rho(int n, const PghrDec* dec, const uint8_t* rho,
+                                                                const uint8_t* status, BA1* mul) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int w = threadIdx.x >> 6;  // wave-uniform
   if (i >= n || status[i] != ZG_STATUS_OK) return;
   const int pj = PGHR_RHO_MUL[w][0], rj = PGHR_RHO_MUL[w][1];
-  const uint8_t* r = rho + (size_t)64 * i + 16 * rj;  // rho2, rho3, rho4, rho5: 16 LE bytes each
+  const uint8_t* r = rho + (size_t)ZG_PGHR_RHO_BYTES * i + 16 * rj;
   uint32_t rw[4];
   for (int l = 0; l < 4; l++)
     rw[l] = (uint32_t)r[4 * l] | ((uint32_t)r[4 * l + 1] << 8) | ((uint32_t)r[4 * l + 2] << 16) |
             ((uint32_t)r[4 * l + 3] << 24);
   const BA1 q = dec[i].pt[pj];
-  mul[8 * (size_t)i + w] = q.inf ? q : bj1_to_aff(bj1_mul(q, rw, 128));
+  mul[ZG_PGHR_NMUL * (size_t)i + w] = q.inf ? q : bj1_to_aff(bj1_mul(q, rw, 128));
 }
 
 // lane per proof: the seven G1 operands of the folded check from the products
-//   P1' = -(a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   P1' = -(rho1 a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
+//   (and P0 = rho1 a: with rho1 random too, one proof's check and the batch's share its operands)
 //   P7  = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a)          (vk.b, gammaBeta1: comb tables)
 __global__ void __launch_bounds__(64) k_pghr_combine(int n, const PghrDec* dec, const BA1* mul, const uint8_t* rho,
                                                       const uint32_t* comb, const uint8_t* status, PghrPts* pts) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != ZG_STATUS_OK) return;
   const PghrDec& d = dec[i];
-  const BA1* m = mul + 8 * (size_t)i;
-  const uint8_t* r = rho + (size_t)64 * i;
+  const BA1* m = mul + ZG_PGHR_NMUL * (size_t)i;
+  const uint8_t* r = rho + (size_t)ZG_PGHR_RHO_BYTES * i;
   PghrPts& o = pts[i];
-  o.p[0] = d.pt[0];
-  BJ1 s = bj1_from(d.pt[1]);
+  o.p[0] = m[8];  // rho1 a
+  BJ1 s = bj1_from(m[9]);  // rho1 a'
   s = bj1_add_aff(s, m[0]);
   s = bj1_add_aff(s, m[1]);
   s = bj1_add_aff(s, m[2]);
@@ -342,10 +349,142 @@ __global__ void __launch_bounds__(128) k_pghr_miller(int n, const PghrPts* pts, 
   fout[(size_t)halves * i + h] = f;
 }
 
+// ---- the batch check (one final exponentiation for the whole call). The per-proof check is
+//   prod_j e(P_ij, Q_j) = 1 with six fixed Q_j (the key's G2 points) and Q_7 = b_i (the proof's);
+// with every weight rho random (rho1 too) the product over proofs of the per-proof checks is
+//   prod_{j<6} e(sum_i P_ij, Q_j) * prod_i e(P_i7, b_i)
+// -- six Miller loops for the batch, one single-pair loop per proof, ONE final exponentiation -- and
+// it equals 1 iff every proof's five equalities hold, but for a probability <= 2^-128 per false
+// one (each equality of each proof carries its own independent 128-bit weight). A batch that fails
+// re-runs the per-proof path (k_pghr_miller + k_fe_*) for the exact statuses.
+// per block (64 proofs): the sums of the six fixed-Q operands over the proofs whose status is OK
+__global__ void __launch_bounds__(64) k_pghr_bsum(int n, const PghrPts* pts, const uint8_t* status, BJ1* part) {
+  __shared__ BJ1 sh[64];
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const bool live = i < n && status[i] == ZG_STATUS_OK;
+  for (int j = 0; j < ZG_BN_FIXED_Q; j++) {
+    sh[threadIdx.x] = live ? bj1_from(pts[i].p[j]) : bj1_inf();
+    __syncthreads();
+    for (int d = 32; d >= 1; d >>= 1) {
+      if ((int)threadIdx.x < d) sh[threadIdx.x] = bj1_add(sh[threadIdx.x], sh[threadIdx.x + d]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(size_t)blockIdx.x * ZG_BN_FIXED_Q + j] = sh[0];
+    __syncthreads();
+  }
+}
+// block j of six: sum_i P_ij over the nb block partials (lanes stride, then an LDS tree) -> agg->p[j];
+// agg->p[6] = infinity (the aggregate has no b pair)
+__global__ void __launch_bounds__(64) k_pghr_bsum_final(int nb, const BJ1* part, PghrPts* agg) {
+  __shared__ BJ1 sh[64];
+  const int j = blockIdx.x, t = threadIdx.x;
+  BJ1 acc = bj1_inf();
+  for (int b = t; b < nb; b += 64) acc = bj1_add(acc, part[(size_t)b * ZG_BN_FIXED_Q + j]);
+  sh[t] = acc;
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    if (t < d) sh[t] = bj1_add(sh[t], sh[t + d]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    agg->p[j] = bj1_to_aff(sh[0]);
+    if (j == 0) {
+      agg->p[6] = {bq_zero(), bq_zero(), true};
+      agg->qb = {b2_one(), b2_one()};  // unused (p[6] infinite); any value keeps the b steps finite
+    }
+  }
+}
+// lane per proof: the single-pair Miller loop e(P_i7, b_i) (the proof's own doubling / addition
+// steps), then the product of the block's 64 values in LDS -> part[block] (1 for proofs that are not OK)
+__global__ void __launch_bounds__(64) k_pghr_bmiller(int n, const PghrPts* pts, const uint8_t* status, Bq12* part) {
+  __shared__ Bq12 sh[64];
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  Bq12 f = b12_one();
+  if (i < n && status[i] == ZG_STATUS_OK && !pts[i].p[6].inf) {
+    const BA2 qb = pts[i].qb;
+    const BA1 p = pts[i].p[6];
+    BH2 t = {qb.x, qb.y, b2_one()};
+    for (int bit = ZG_BN_ATE_BITS - 2; bit >= -2; bit--) {
+      const int nsub = bit >= 0 ? (bn_ate_bit(bit) ? 2 : 1) : 1;
+      if (bit >= 0) f = b12_sqr(f);
+      for (int s = 0; s < nsub; s++) {
+        BLine l;
+        if (bit >= 0)
+          l = s == 0 ? bh2_dbl_step(&t) : bh2_add_step(&t, qb);
+        else if (bit == -1)
+          l = bh2_add_step(&t, ba2_frob(qb));
+        else {
+          const BA2 q2 = ba2_frob2(qb);
+          l = bh2_add_step(&t, {q2.x, b2_neg(q2.y)});
+        }
+        f = b12_mul_bline(f, l, p);
+      }
+    }
+  }
+  sh[threadIdx.x] = f;
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    if ((int)threadIdx.x < d) sh[threadIdx.x] = b12_mul(sh[threadIdx.x], sh[threadIdx.x + d]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+// the six fixed pairs' Miller loop on the batch's sums, split by loop position (a lone lane carrying
+// all six took 39 ms, as long as the whole per-proof loop at 64k): lane (h, j) runs pair j over
+// segment h of the loop's 66 positions (bits 63..0 -- a doubling step and an addition when set --
+// then the pi(Q), -pi^2(Q) additions) from f = 1, and the block multiplies each segment's six pair
+// values in LDS -> seg[h]. The loop's value is the Horner product over the segments
+//   (((seg[0])^(2^sq(1)) seg[1])^(2^sq(2)) ...) seg[S-1],  sq(h) = the doublings of segment h
+// which k_pghr_fe_coop forms after k_fe_easy's map x -> x^((p^6 - 1)(p^2 + 1)) (a homomorphism) has
+// put every seg[h] in the cyclotomic subgroup, where a squaring is Granger-Scott's.
+#define ZG_PGHR_FSEG 8
+#define ZG_FE_SLOTS 6  // the final exponentiation's per-value HBM workspace (k_fe_easy below)
+#define ZG_BN_POS (ZG_BN_ATE_BITS + 1)  // loop positions: q = 0 is bit 63, q = 64, 65 the two additions
+static_assert(ZG_PGHR_FSEG * ZG_BN_FIXED_Q <= 64, "one lane per (segment, pair)");
+ZG_INL int pghr_pos_bit(int q) { return ZG_BN_ATE_BITS - 2 - q; }
+ZG_INL int pghr_seg_lo(int h) { return h * ZG_BN_POS / ZG_PGHR_FSEG; }
+ZG_INL int pghr_seg_sq(int h) {  // doubling steps (squarings of f) in segment h
+  int sq = 0;
+  for (int q = pghr_seg_lo(h); q < pghr_seg_lo(h + 1); q++) sq += pghr_pos_bit(q) >= 0;
+  return sq;
+}
+__global__ void __launch_bounds__(64) k_pghr_fseg(const PghrPts* agg, const BLine* lines, Bq12* seg) {
+  __shared__ Bq12 sh[64];
+  const int t = threadIdx.x, h = t / ZG_BN_FIXED_Q, j = t % ZG_BN_FIXED_Q;
+  Bq12 f = b12_one();
+  if (h < ZG_PGHR_FSEG && !agg->p[j].inf) {
+    const BA1 p = agg->p[j];
+    const int q0 = pghr_seg_lo(h), q1 = pghr_seg_lo(h + 1);
+    int li = 0;
+    for (int q = 0; q < q0; q++) {
+      const int bit = pghr_pos_bit(q);
+      li += bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
+    }
+    for (int q = q0; q < q1; q++) {
+      const int bit = pghr_pos_bit(q);
+      if (bit >= 0 && q > q0) f = b12_sqr(f);  // the segment's first squaring is of 1 (counted in sq(h))
+      const int nsub = bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
+      for (int s = 0; s < nsub; s++, li++) f = b12_mul_bline(f, lines[(size_t)j * ZG_BN_NLINES + li], p);
+    }
+  }
+  sh[t] = f;
+  __syncthreads();
+  const bool seg_lane = h < ZG_PGHR_FSEG;
+  if (seg_lane && (j & 1) == 0) sh[t] = b12_mul(sh[t], sh[t + 1]);  // (01)(23)(45)
+  __syncthreads();
+  if (seg_lane && j == 0) seg[h] = b12_mul(b12_mul(sh[t], sh[t + 2]), sh[t + 4]);
+}
+// one level of the product tree over the block products: dst[k] = src[2k] * src[2k + 1] (an odd
+// last one moves up)
+__global__ void __launch_bounds__(64) k_bn_tree(const Bq12* src, Bq12* dst, int m) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (m + 1) / 2) return;
+  dst[k] = 2 * k + 1 < m ? b12_mul(src[2 * k], src[2 * k + 1]) : src[2 * k];
+}
+
 // the final exponentiation of zg_bn254.h bn_final_exp, split so that no kernel holds more than
 // a few Fq12 values at once (a lane-per-proof Fq12 is 96 VGPRs): the chain's intermediates live in
 // a per-proof HBM workspace w[0..5] = t, b, d, e, g, (spare)
-#define ZG_FE_SLOTS 6
 // halves 2: f holds two partial Miller products per proof (k_pghr_miller), multiplied here
 __global__ void __launch_bounds__(64) k_fe_easy(int n, const Bq12* f, const uint8_t* status, Bq12* w, int halves) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -386,6 +525,166 @@ __global__ void __launch_bounds__(64) k_fe_last(int n, uint8_t* status, Bq12* w)
   r = b12_mul(b12_frob(s[5], 2), r);                   // r
   r = b12_mul(b12_frob(b12_mul(b12_conj(s[0]), s[4]), 3), r);
   status[i] = b12_is_one(r) ? ZG_STATUS_OK : ZG_STATUS_VERIFY_FAILED;
+}
+
+// ---- the batch check's one final exponentiation on one wave. As a lane-serial chain (k_fe_exp on
+// one lane) its three exponentiations by -u took 12 ms; here an Fq12 lives in LDS as its six Fq2
+// coefficients by power of w (z[e], e = a + 2b for the tower's c_a.c_b: z[0] = c0.c0, z[2] = c0.c1,
+// z[4] = c0.c2, z[1] = c1.c0, z[3] = c1.c1, z[5] = c1.c2) and each operation spreads its Fq
+// products over the wave's lanes, then six lanes form the coefficients:
+//   mul   the 36 Fq2 products z_i z'_j (Karatsuba, 3 Fq products each: 108 on 64 lanes, two rounds);
+//         out[e] = the sum over i + j = e (mod 6), those with i + j >= 6 times xi (w^6 = v^3 = xi)
+//   csqr  Granger-Scott (b12_csqr): the pairs (z[p], z[p + 3]) give A B and (A + B)(xi B + A), 6 Fq2
+//         products = 18 Fq products, one round
+//   conj, frob, copy  lane e on z[e]
+// A product then costs about two Fq products of latency and a cyclotomic squaring one, against 54 and
+// 18 on one lane. The chain is bn_final_exp's (zg_bn254.h; oracle.bn254.final_exponentiation_fc).
+struct BcF12 {
+  Bq2 z[6];
+};
+#define ZG_BC_SLOTS 8
+struct BcWS {
+  BcF12 s[ZG_BC_SLOTS];
+  Bq m[108];
+};
+ZG_INL int bc_tower(int e) { return (e & 1) * 3 + (e >> 1); }  // index of z[e] among Bq12's six Bq2
+__device__ void bc_load(BcWS* ws, int dst, const Bq12* x) {
+  const int e = threadIdx.x;
+  if (e < 6) ws->s[dst].z[e] = reinterpret_cast<const Bq2*>(x)[bc_tower(e)];
+  __syncthreads();
+}
+__device__ void bc_mul(BcWS* ws, int dst, int a, int b) {
+  for (int t = threadIdx.x; t < 108; t += 64) {
+    const int k = t / 3, m = t - 3 * k, i = k / 6, j = k - 6 * i;
+    const Bq2 x = ws->s[a].z[i], y = ws->s[b].z[j];
+    const Bq u = m == 0 ? x.c0 : m == 1 ? x.c1 : bq_add(x.c0, x.c1);
+    const Bq v = m == 0 ? y.c0 : m == 1 ? y.c1 : bq_add(y.c0, y.c1);
+    ws->m[t] = bq_mul(u, v);
+  }
+  __syncthreads();
+  const int e = threadIdx.x;
+  if (e < 6) {
+    Bq2 lo = b2_zero(), hi = b2_zero();
+    for (int i = 0; i < 6; i++) {
+      const int j = (e - i + 6) % 6, k = 6 * i + j;
+      const Bq m0 = ws->m[3 * k], m1 = ws->m[3 * k + 1], m2 = ws->m[3 * k + 2];
+      const Bq2 q = {bq_sub(m0, m1), bq_sub(bq_sub(m2, m0), m1)};
+      if (i + j >= 6)
+        hi = b2_add(hi, q);
+      else
+        lo = b2_add(lo, q);
+    }
+    ws->s[dst].z[e] = b2_add(lo, b2_mul_xi(hi));
+  }
+  __syncthreads();
+}
+__device__ void bc_csqr(BcWS* ws, int dst, int a) {
+  const int t = threadIdx.x;
+  if (t < 18) {
+    const int q = t / 3, m = t - 3 * q, pr = q >> 1;
+    const Bq2 A = ws->s[a].z[pr], B = ws->s[a].z[pr + 3];
+    const Bq2 x = (q & 1) ? b2_add(A, B) : A, y = (q & 1) ? b2_add(b2_mul_xi(B), A) : B;
+    const Bq u = m == 0 ? x.c0 : m == 1 ? x.c1 : bq_add(x.c0, x.c1);
+    const Bq v = m == 0 ? y.c0 : m == 1 ? y.c1 : bq_add(y.c0, y.c1);
+    ws->m[t] = bq_mul(u, v);
+  }
+  __syncthreads();
+  const int e = t;
+  if (e < 6) {
+    // pair of z[e]: (z0, z3) -> 0, (z2, z5) -> 1, (z4, z1) -> 2
+    const int pr = (e & 1) ? ((e + 3) % 6) / 2 : e / 2;
+    auto prod = [&](int q) {
+      const Bq m0 = ws->m[3 * q], m1 = ws->m[3 * q + 1], m2 = ws->m[3 * q + 2];
+      return Bq2{bq_sub(m0, m1), bq_sub(bq_sub(m2, m0), m1)};
+    };
+    const Bq2 ab = prod(2 * pr), z = ws->s[a].z[e];
+    Bq2 r;
+    if ((e & 1) == 0) {  // 3 t0 - 2 z, t0 = (A + B)(xi B + A) - A B - xi A B
+      const Bq2 t0 = b2_sub(b2_sub(prod(2 * pr + 1), ab), b2_mul_xi(ab));
+      const Bq2 d = b2_sub(t0, z);
+      r = b2_add(b2_add(d, d), t0);
+    } else {  // 3 t1 + 2 z, t1 = 2 A B (times xi for z[1])
+      Bq2 t1 = b2_add(ab, ab);
+      if (e == 1) t1 = b2_mul_xi(t1);
+      const Bq2 d = b2_add(t1, z);
+      r = b2_add(b2_add(d, d), t1);
+    }
+    ws->s[dst].z[e] = r;
+  }
+  __syncthreads();
+}
+__device__ void bc_copy(BcWS* ws, int dst, int a, bool conj) {
+  const int e = threadIdx.x;
+  if (e < 6) {
+    const Bq2 x = ws->s[a].z[e];
+    ws->s[dst].z[e] = conj && (e & 1) ? b2_neg(x) : x;
+  }
+  __syncthreads();
+}
+__device__ void bc_frob(BcWS* ws, int dst, int a, int k) {
+  const int e = threadIdx.x;
+  if (e < 6) {
+    Bq2 x = ws->s[a].z[e];
+    if (k & 1) x = b2_conj(x);
+    if (e) {
+      const uint32_t* const g[3][5] = {{BQ_FROB1_1, BQ_FROB1_2, BQ_FROB1_3, BQ_FROB1_4, BQ_FROB1_5},
+                                       {BQ_FROB2_1, BQ_FROB2_2, BQ_FROB2_3, BQ_FROB2_4, BQ_FROB2_5},
+                                       {BQ_FROB3_1, BQ_FROB3_2, BQ_FROB3_3, BQ_FROB3_4, BQ_FROB3_5}};
+      x = b2_mul(x, b2_c(g[k - 1][e - 1]));
+    }
+    ws->s[dst].z[e] = x;
+  }
+  __syncthreads();
+}
+// dst = src^-u (src cyclotomic); tmp != src, dst
+__device__ void bc_exp_by_neg_u(BcWS* ws, int dst, int src, int tmp) {
+  bc_copy(ws, tmp, src, false);
+  for (int i = 61; i >= 0; i--) {
+    bc_csqr(ws, tmp, tmp);
+    if ((BN_U >> i) & 1ull) bc_mul(ws, tmp, tmp, src);
+  }
+  bc_copy(ws, dst, tmp, true);
+}
+// w: slot 0 of lanes 0..S of k_fe_easy's workspace (the segments' values and the b pairs' product,
+// each mapped into the cyclotomic subgroup) -> the Horner product (k_pghr_fseg's note), its hard part,
+// status[0] = OK iff the result is 1
+__global__ void __launch_bounds__(64) k_pghr_fe_coop(const Bq12* w, uint8_t* status) {
+  __shared__ BcWS ws;
+  enum { T, B, D, E, G, X, Y, Z };
+  bc_load(&ws, T, w);
+  for (int h = 1; h <= ZG_PGHR_FSEG; h++) {
+    const int sq = h < ZG_PGHR_FSEG ? pghr_seg_sq(h) : 0;
+    for (int k = 0; k < sq; k++) bc_csqr(&ws, T, T);
+    bc_load(&ws, X, w + (size_t)ZG_FE_SLOTS * h);
+    bc_mul(&ws, T, T, X);
+  }
+  bc_exp_by_neg_u(&ws, X, T, Y);  // a = t^-u
+  bc_csqr(&ws, B, X);             // b = a^2
+  bc_csqr(&ws, X, B);             // c = b^2
+  bc_mul(&ws, D, X, B);           // d = c b
+  bc_exp_by_neg_u(&ws, E, D, Y);  // e = d^-u
+  bc_csqr(&ws, X, E);
+  bc_exp_by_neg_u(&ws, G, X, Y);  // g = (e^2)^-u
+  bc_copy(&ws, X, G, true);
+  bc_mul(&ws, X, X, E);
+  bc_copy(&ws, Y, D, true);
+  bc_mul(&ws, G, X, Y);           // k = g^-1 e d^-1 (in G)
+  bc_mul(&ws, X, G, B);           // l = k b
+  bc_mul(&ws, Y, G, E);
+  bc_mul(&ws, Y, T, Y);           // n = t k e
+  bc_frob(&ws, Z, X, 1);
+  bc_mul(&ws, Z, Z, Y);           // l^p n
+  bc_frob(&ws, B, G, 2);
+  bc_mul(&ws, Z, B, Z);           // k^(p^2) l^p n
+  bc_copy(&ws, Y, T, true);
+  bc_mul(&ws, Y, Y, X);
+  bc_frob(&ws, Y, Y, 3);          // (t^-1 l)^(p^3)
+  bc_mul(&ws, Y, Y, Z);
+  if (threadIdx.x == 0) {
+    bool one = b2_eq(ws.s[Y].z[0], b2_one());
+    for (int e = 1; e < 6; e++) one = one && b2_is_zero(ws.s[Y].z[e]);
+    status[0] = one ? ZG_STATUS_OK : ZG_STATUS_VERIFY_FAILED;
+  }
 }
 
 // zg_bn254_pairing (tests): the Miller loop of e(P, Q) -> f; the final exponentiation then runs
@@ -597,7 +896,8 @@ int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, cons
 
 int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
                      const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
-                     std::string* err) {
+                     bool* batch_failed, std::string* err) {
+  if (batch_failed) *batch_failed = false;
   if (!n) return ZG_OK;
   // device buffers of this call
   struct Bufs {
@@ -616,7 +916,7 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   Bq12* df;
   BCHK(alloc((void**)&dp, 296 * n));
   BCHK(alloc((void**)&din, 9 * 32 * n));
-  BCHK(alloc((void**)&drho, 64 * n));
+  BCHK(alloc((void**)&drho, ZG_PGHR_RHO_BYTES * n));
   BCHK(alloc((void**)&dst, n));
   BCHK(alloc((void**)&dpts, sizeof(PghrPts) * n));
   PghrDec* ddec;
@@ -624,7 +924,7 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   BJ1* daccp;
   uint8_t* dokb;
   BCHK(alloc((void**)&ddec, sizeof(PghrDec) * n));
-  BCHK(alloc((void**)&dmul, sizeof(BA1) * 8 * n));
+  BCHK(alloc((void**)&dmul, sizeof(BA1) * ZG_PGHR_NMUL * n));
   BCHK(alloc((void**)&daccp, sizeof(BJ1) * 9 * n));
   BCHK(alloc((void**)&dokb, 8 * n));
   BCHK(alloc((void**)&df, sizeof(Bq12) * 2 * n));
@@ -632,7 +932,7 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   BCHK(alloc((void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n));
   BCHK(hipMemcpyAsync(dp, proofs, 296 * n, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(din, inputs, 9 * 32 * n, hipMemcpyHostToDevice, st));
-  BCHK(hipMemcpyAsync(drho, rho, 64 * n, hipMemcpyHostToDevice, st));
+  BCHK(hipMemcpyAsync(drho, rho, ZG_PGHR_RHO_BYTES * n, hipMemcpyHostToDevice, st));
   if (ninputs) {
     BCHK(alloc((void**)&dni, n));
     BCHK(hipMemcpyAsync(dni, ninputs, n, hipMemcpyHostToDevice, st));
@@ -652,24 +952,59 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, din, dni, d->vk, dokb, daccp, ddec,
                      dst);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_rho, dim3(bn_blocks(n)), dim3(512), 0, st, (int)n, ddec, drho, dst, dmul);
+  hipLaunchKernelGGL(k_pghr_rho, dim3(bn_blocks(n)), dim3(64 * ZG_PGHR_NMUL), 0, st, (int)n, ddec, drho, dst, dmul);
   BCHK(hipGetLastError());
   hipLaunchKernelGGL(k_pghr_combine, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
   BCHK(hipGetLastError());
-  const int halves = n < ZG_PGHR_SPLIT_BELOW ? 2 : 1;
-  hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df,
-                     halves);
+  // the batch check: six Miller loops on the sums, one single-pair loop per proof, one final exponentiation
+  const unsigned nb = bn_blocks(n);
+  BJ1* dpart;
+  PghrPts* dagg;
+  Bq12 *dbmil, *dbtmp, *dseg, *dbw;
+  uint8_t* dbst;
+  BCHK(alloc((void**)&dpart, sizeof(BJ1) * ZG_BN_FIXED_Q * nb));
+  BCHK(alloc((void**)&dagg, sizeof(PghrPts)));
+  BCHK(alloc((void**)&dbmil, sizeof(Bq12) * nb));
+  BCHK(alloc((void**)&dbtmp, sizeof(Bq12) * ((nb + 1) / 2)));
+  BCHK(alloc((void**)&dseg, sizeof(Bq12) * (ZG_PGHR_FSEG + 1)));
+  BCHK(alloc((void**)&dbw, sizeof(Bq12) * ZG_FE_SLOTS * (ZG_PGHR_FSEG + 1)));
+  BCHK(alloc((void**)&dbst, ZG_PGHR_FSEG + 1));
+  BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, st));
+  hipLaunchKernelGGL(k_pghr_bsum, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dpart);
+  hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, st, (int)nb, dpart, dagg);
+  hipLaunchKernelGGL(k_pghr_bmiller, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dbmil);
+  Bq12 *src = dbmil, *dstb = dbtmp;
+  for (int m = (int)nb; m > 1; m = (m + 1) / 2) {
+    hipLaunchKernelGGL(k_bn_tree, dim3(bn_blocks((m + 1) / 2)), dim3(64), 0, st, src, dstb, m);
+    std::swap(src, dstb);
+  }
+  BCHK(hipMemcpyAsync(dseg + ZG_PGHR_FSEG, src, sizeof(Bq12), hipMemcpyDeviceToDevice, st));
+  // the fixed pairs' loop on the sums by segments -> dseg[0..S); the easy part of all S + 1 values,
+  // their Horner product, the hard part of that one value
+  hipLaunchKernelGGL(k_pghr_fseg, dim3(1), dim3(64), 0, st, dagg, d->lines, dseg);
+  hipLaunchKernelGGL(k_fe_easy, dim3(1), dim3(64), 0, st, ZG_PGHR_FSEG + 1, dseg, dbst, dbw, 1);
+  hipLaunchKernelGGL(k_pghr_fe_coop, dim3(1), dim3(64), 0, st, dbw, dbst);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw, halves);
-  BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_exp<1>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
-  BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_exp<2>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
-  BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_exp<3>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
-  BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_fe_last, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
-  BCHK(hipGetLastError());
+  uint8_t bok = 0;
+  BCHK(hipMemcpyAsync(&bok, dbst, 1, hipMemcpyDeviceToHost, st));
+  BCHK(hipStreamSynchronize(st));
+  if (batch_failed) *batch_failed = bok != ZG_STATUS_OK;
+  if (bok != ZG_STATUS_OK) {  // some proof fails: the per-proof path for the exact statuses
+    const int halves = n < ZG_PGHR_SPLIT_BELOW ? 2 : 1;
+    hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df,
+                       halves);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw, halves);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_exp<1>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_exp<2>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_exp<3>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_fe_last, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    BCHK(hipGetLastError());
+  }
   if (kernel_ms) BCHK(hipEventRecord(e1, st));
   BCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, st));
   BCHK(hipStreamSynchronize(st));
