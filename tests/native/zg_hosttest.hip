@@ -148,6 +148,20 @@ int zgt_bn_g2_membership(const uint8_t* x0, const uint8_t* x1, const uint8_t* y0
   return 1;
 }
 
+// BN254 G1 GLV: res[0] = [a + b lambda] q (bj1_mul_glv, k = a || b as 16 LE bytes) equals [s] q for
+// the 32-byte LE scalar s; res[1] = phi(q) equals [lambda] q (BN_LAMBDA)
+int zgt_bn_glv_check(const uint8_t* qx, const uint8_t* qy, const uint8_t* k, const uint8_t* s, int* res) {
+  const BA1 q = {ld_bq(qx), ld_bq(qy), false};
+  if (!ba1_on_curve(q)) return 0;
+  uint32_t kw[4], sw[8];
+  for (int l = 0; l < 4; l++) kw[l] = (uint32_t)k[4 * l] | ((uint32_t)k[4 * l + 1] << 8) | ((uint32_t)k[4 * l + 2] << 16) | ((uint32_t)k[4 * l + 3] << 24);
+  for (int l = 0; l < 8; l++) sw[l] = (uint32_t)s[4 * l] | ((uint32_t)s[4 * l + 1] << 8) | ((uint32_t)s[4 * l + 2] << 16) | ((uint32_t)s[4 * l + 3] << 24);
+  auto eq = [](const BA1& a, const BA1& b) { return a.inf == b.inf && (a.inf || (bq_eq(a.x, b.x) && bq_eq(a.y, b.y))); };
+  res[0] = eq(bj1_to_aff(bj1_mul_glv(q, kw)), bj1_to_aff(bj1_mul(q, sw, 256)));
+  res[1] = eq(ba1_phi(q), bj1_to_aff(bj1_mul(q, BN_LAMBDA, 256)));
+  return 1;
+}
+
 int zgt_bn_g1_decode(const uint8_t* in, uint8_t* out) {
   BA1 p;
   if (!bn_g1_decode(in, &p)) return 0;

@@ -126,3 +126,25 @@ def test_host_g2_membership_psi_equals_order_check():
         res = (ctypes.c_int * 2)()
         assert L.zgt_bn_g2_membership(b32(x[0]), b32(x[1]), b32(y[0]), b32(y[1]), res) == 1
         assert res[0] == res[1] == int(want)
+
+
+def test_host_g1_glv_weights():
+    """the batch check's weights rho = a + b lambda (zg_pghr13.hip k_pghr_rho, zg_bn254.h bj1_mul_glv):
+    the joint 64-bit double-and-add over q and phi(q) equals [a + b lambda mod r] q, and phi(q) =
+    (beta x, y) is [lambda] q, on random G1 points and edge halves (0, all-ones)"""
+    import ctypes
+    import random
+    from oracle import bn254 as BN
+    from tests import hostlib
+    L = hostlib.lib()
+    lam = 0xb3c4d79d41a917585bfc41088d8daaa78b17ea66b99c90dd
+    rng = random.Random(31)
+    b32 = lambda v: v.to_bytes(32, "little")
+    halves = [(0, 1), (1, 0), (2**64 - 1, 2**64 - 1), (0, 2**64 - 1)] + \
+             [(rng.getrandbits(64), rng.getrandbits(64)) for _ in range(6)]
+    for a, b in halves:
+        q = BN.ec_mul(BN._F1, BN.G1_GEN, rng.randrange(1, BN.R))
+        res = (ctypes.c_int * 2)()
+        k = a.to_bytes(8, "little") + b.to_bytes(8, "little")
+        assert L.zgt_bn_glv_check(b32(q[0]), b32(q[1]), k, b32((a + b * lam) % BN.R), res) == 1
+        assert list(res) == [1, 1], (a, b)

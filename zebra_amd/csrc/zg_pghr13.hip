@@ -125,7 +125,8 @@ __global__ void __launch_bounds__(64) k_bn_comb(const BnVK* vk, uint32_t* table)
 }
 
 // [s] base_j from the comb table (s: nbytes little-endian bytes)
-ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s, int nbytes) {
+// phi: the table's points mapped by the G1 endomorphism (beta x, y), i.e. [s lambda] of the base
+ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s, int nbytes, bool phi = false) {
   for (int w = 0; w < nbytes; w++) {
     const int d = s[w];
     if (!d) continue;
@@ -136,6 +137,7 @@ ZG_INL BJ1 bn_comb_mul(BJ1 acc, const uint32_t* comb, int base, const uint8_t* s
       p.y.l[l] = e[8 + l];
     }
     p.inf = false;
+    if (phi) p.x = bq_mul(p.x, bq_c(BQ_BETA));
     acc = bj1_add_aff(acc, p);
   }
   return acc;
@@ -235,10 +237,11 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* inputs, 
   status[i] = ZG_STATUS_OK;
 }
 
-// the eight 128-bit products rho_j Q of a proof, one per wave of a 512-lane block (64 proofs):
-// wave w computes PGHR_RHO_MUL[w] = (point, rho index), affine, -> mul[8 i + w]. One lane per
-// proof ran them back to back (eight 128-bit double-and-add chains at one wave per SIMD).
-#define ZG_PGHR_RHO_BYTES 80  // rho2, rho3, rho4, rho5, rho1: 16 LE bytes each
+// the ten products rho_j Q of a proof, one per wave of a 640-lane block (64 proofs): wave w computes
+// PGHR_RHO_MUL[w] = (point, rho index), affine, -> mul[10 i + w]. A weight is rho = a + b lambda mod r
+// for its 16 random bytes a (LE 0..7), b (8..15) -- 2^128 distinct values (zg_bn254.h bj1_mul_glv) --
+// so each product is a 64-bit joint double-and-add over q and phi(q).
+#define ZG_PGHR_RHO_BYTES 80  // rho2, rho3, rho4, rho5, rho1: (a, b) 16 LE bytes each
 #define ZG_PGHR_NMUL 10
 __device__ __constant__ const int8_t PGHR_RHO_MUL[ZG_PGHR_NMUL][2] = {
     {2, 0},  // rho2 b'
@@ -264,7 +267,7 @@ __global__ void __launch_bounds__(64 * ZG_PGHR_NMUL) k_pghr_rho(int n, const Pgh
     rw[l] = (uint32_t)r[4 * l] | ((uint32_t)r[4 * l + 1] << 8) | ((uint32_t)r[4 * l + 2] << 16) |
             ((uint32_t)r[4 * l + 3] << 24);
   const BA1 q = dec[i].pt[pj];
-  mul[ZG_PGHR_NMUL * (size_t)i + w] = q.inf ? q : bj1_to_aff(bj1_mul(q, rw, 128));
+  mul[ZG_PGHR_NMUL * (size_t)i + w] = q.inf ? q : bj1_to_aff(bj1_mul_glv(q, rw));
 }
 
 // lane per proof: the seven G1 operands of the folded check from the products
@@ -289,8 +292,10 @@ __global__ void __launch_bounds__(64) k_pghr_combine(int n, const PghrDec* dec, 
   o.p[3] = m[4];
   o.p[4] = d.pt[8].inf ? d.pt[8] : ba1_neg(m[5]);
   o.p[5] = ba1_neg(m[6]);
-  BJ1 t = bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC, r, 16);
-  const BA1 g4 = bj1_to_aff(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 16));
+  // rho G = a G + b phi(G) for the comb tables' fixed G: the halves' byte windows, phi on the b half
+  BJ1 t = bn_comb_mul(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC, r, 8), comb, ZG_BN_MAX_IC, r + 8, 8, true);
+  const BA1 g4 = bj1_to_aff(
+      bn_comb_mul(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 8), comb, ZG_BN_MAX_IC + 1, r + 40, 8, true));
   t = bj1_add_aff(t, ba1_neg(g4));
   if (!d.pt[7].inf) t = bj1_add_aff(t, m[7]);
   o.p[6] = bj1_to_aff(t);
