@@ -136,7 +136,8 @@ def test_gpu_pghr13_keys_per_context():
 @pytest.mark.gpu
 def test_gpu_pghr13_batch_check_paths(ctx):
     """the one-check-per-call path (zg_pghr13.hip: the key pairs on the batch's sums, one single-pair
-    loop per proof, one final exponentiation): 2,048 valid proofs, then the same with decode-invalid
+    loop per proof split by segments, one final exponentiation): 2,061 valid proofs (33 blocks, the
+last one partial: odd product trees), also through the packed buffers, then the same with decode-invalid
     and non-canonical cases mixed in (excluded from the batch, which still passes), then with one
     VERIFY_FAILED proof (the batch fails and the per-proof path gives the exact statuses)"""
     from zebra_amd import zg
@@ -146,7 +147,7 @@ def test_gpu_pghr13_batch_check_paths(ctx):
     failing = [c for c in cases if c["status"] == zg.STATUS_VERIFY_FAILED]
     assert valid and skipped and failing
     rnd = random.Random(9)
-    base = [valid[rnd.randrange(len(valid))] for _ in range(2048)]
+    base = [valid[rnd.randrange(len(valid))] for _ in range(2061)]
     for extra, fails in (([], 0), (skipped, 0), (skipped + failing[:1], 1)):
         batch = list(base)
         for c in extra:
@@ -159,3 +160,9 @@ def test_gpu_pghr13_batch_check_paths(ctx):
         # the batch check alone decides an all-valid call (a wrong batch check would only show here:
         # the per-proof path would still give the right statuses)
         assert st1["pghr13_batch_failures"] - st0["pghr13_batch_failures"] == fails
+        if not extra:  # the ABI's packed buffers give the same
+            ins = [_inputs(c) for c in batch]
+            packed = ctx.pghr13_verify(b"".join(bytes.fromhex(c["proof"]) for c in batch),
+                                       b"".join(b"".join(r) + bytes(32 * (9 - len(r))) for r in ins),
+                                       bytes(len(r) for r in ins))
+            assert packed == got

@@ -55,6 +55,31 @@ for s in $STEPS; do
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pghr -o run -- python3 $R/tools/bench_pghr13.py --no-cpu --reps 2 > /dev/null 2> $O/prof_pghr.err || { echo "rocprof pghr failed"; tail -30 $O/prof_pghr.err; exit 1; }
     cd $R && python3 tools/rocpd_stats.py $O/prof_pghr/run_results.db $O/kernel_stats_pghr.csv && rm -f $O/prof_pghr/run_results.db ;;
+  pghrvar)
+    for v in $VARIANTS; do for n in 65536 8192; do
+      ZG_LIB_VARIANT=$v timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n $n > $O/pghr_${v}_$n.json 2> $O/pghr_${v}_$n.err || { echo "pghr bench $v failed"; tail -30 $O/pghr_${v}_$n.err; exit 1; }
+      echo "$v $(cat $O/pghr_${v}_$n.json)"
+    done; done ;;
+  pghrk)
+    for v in main $VARIANTS; do for k in 1 2 4 8; do
+      lv=$v; [ $v = main ] && lv=
+      ZG_LIB_VARIANT=$lv ZG_BSEG_K=$k timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n 65536 > $O/pghrk_${v}_$k.json 2> $O/pghrk_${v}_$k.err || { echo "pghr bench $v $k failed"; tail -30 $O/pghrk_${v}_$k.err; exit 1; }
+      echo "$v K=$k $(cat $O/pghrk_${v}_$k.json)"
+    done; done ;;
+  pghrtests)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_pghr13.py tests/test_collector.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_pghr.log 2>&1 || { echo "gpu pghr tests failed"; tail -60 $O/gpu_tests_pghr.log; exit 1; }
+    tail -3 $O/gpu_tests_pghr.log ;;
+  c2trace)
+    timeout -k 10 200 python3 -u tools/config2_trace.py > $O/c2.json 2> $O/c2.err || { echo "config2 failed"; tail -30 $O/c2.err; exit 1; }
+    cat $O/c2.json
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run -- python3 $R/tools/config2_trace.py > $O/prof_c2.json 2> $O/prof_c2.err || { echo "rocprof c2 failed"; tail -30 $O/prof_c2.err; exit 1; }
+    cd $R && python3 tools/timeline.py $O/prof_c2/run_results.db k_chacha20 $O/c2_timeline.txt > /dev/null && python3 tools/rocpd_stats.py $O/prof_c2/run_results.db $O/kernel_stats_c2.csv && rm -f $O/prof_c2/run_results.db ;;
+  bisect)
+    for B in 512 1024 2048; do
+      ZG_BISECT_BUDGET=$B timeout -k 10 300 python3 -u tools/small_batch.py 3 > $O/small_b$B.json 2> $O/small_b$B.err || { echo "small batch $B failed"; tail -30 $O/small_b$B.err; exit 1; }
+      python3 -c "import json; d=[json.loads(l) for l in open('$O/small_b$B.json') if l.startswith('{')]; print('budget $B', [(r['cap'], round(r['config2_1024_spends']['ms_per_batch'],2), round(r['config4_4096_1pct_corrupted']['ms_per_batch'],2), r['config4_4096_1pct_corrupted']['exact_reject_set'], r['stats']['bisect_nodes']) for r in d])"
+    done ;;
   prof8k)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 36 --warmup 0 > $O/prof8k_bench.json 2> $O/prof8k_bench.err || { echo "rocprof 8k failed"; tail -30 $O/prof8k_bench.err; exit 1; }

@@ -53,9 +53,9 @@ struct BnKey;
 BnDev* bn_dev_new();
 void bn_dev_free(BnDev* d);
 int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, const BnKey** out, std::string* err);
-int bn_pghr13_verify(const BnKey* k, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
-                     const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
-                     bool* batch_failed, std::string* err);
+int bn_pghr13_verify(const BnKey* k, hipStream_t st, hipStream_t side, size_t n, const uint8_t* proofs,
+                     const uint8_t* inputs, const uint8_t* ninputs, const uint8_t* rho, uint8_t* status,
+                     float* kernel_ms, bool* batch_failed, void** arena, size_t* arena_cap, std::string* err);
 int bn_pairing(hipStream_t st, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt, std::string* err);
 }  // namespace zg
 
@@ -163,6 +163,8 @@ struct zg_ctx {
   const zg::BnKey* bn_key = nullptr;  // this slot's PGHR13 key (an immutable entry of the device cache)
   void* tree_arena = nullptr;  // zg_tree_roots scratch (grow-only, zg_merkle.hip)
   size_t tree_arena_cap = 0;
+  void* bn_arena = nullptr;  // zg_pghr13_verify scratch (grow-only, zg_pghr13.hip)
+  size_t bn_arena_cap = 0;
 };
 
 static int fail(zg_ctx* c, int code, const std::string& msg) {
@@ -334,7 +336,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
                   ctx->msm.entries, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
-                  ctx->d_dbg};
+                  ctx->bn_arena, ctx->d_dbg};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int i = 0; i < ZG_NEV; i++)
@@ -1043,6 +1045,10 @@ static int build_trees(zg_ctx* ctx) {
 // exponentiations, latency-bound), so few failing nodes descend many levels at once. E.g.
 // 4,096 proofs with 27 failing: 512 nodes of 8, then 216 leaves.
 #define ZG_BISECT_BUDGET 512
+static size_t bisect_budget() {  // ZG_BISECT_BUDGET=<nodes> overrides (tuning)
+  static const long v = getenv("ZG_BISECT_BUDGET") ? atol(getenv("ZG_BISECT_BUDGET")) : 0;
+  return v >= 16 ? (size_t)v : (size_t)ZG_BISECT_BUDGET;
+}
 static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st, bool root_failed) {
   const int npad = (int)ctx->npad, n = (int)ctx->n;
   int depth_leaf = 0;
@@ -1063,11 +1069,12 @@ static int bisect(zg_ctx* ctx, std::vector<uint8_t>& st, bool root_failed) {
   int d = 0;  // depth of the failing nodes
   while (!fails.empty() && d < depth_leaf) {
     int k = 1;
-    while (k < depth_leaf - d && fails.size() * (size_t)(2 << k) <= ZG_BISECT_BUDGET) k++;
+    const size_t budget = bisect_budget();
+    while (k < depth_leaf - d && fails.size() * (size_t)(2 << k) <= budget) k++;
     // four proofs per lane wrote no pair-level nodes: go from the quad level (or above) straight
     // to the leaves, or stop one level higher
     if (ctx->quads_last && d + k == depth_leaf - 1) {
-      if (k > 1 && fails.size() * (size_t)(2 << (k + 1)) > ZG_BISECT_BUDGET)
+      if (k > 1 && fails.size() * (size_t)(2 << (k + 1)) > budget)
         k--;
       else
         k++;
@@ -1587,8 +1594,8 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
     return fail(ctx, ZG_E_INVAL, "getrandom failed");
   }
   bool batch_failed = false;
-  const int rc = bn_pghr13_verify(ctx->bn_key, ctx->stream, n, proofs, inputs, n_inputs, rho.data(), status,
-                                  kernel_ms, &batch_failed, &ctx->err);
+  const int rc = bn_pghr13_verify(ctx->bn_key, ctx->stream, ctx->side, n, proofs, inputs, n_inputs, rho.data(),
+                                  status, kernel_ms, &batch_failed, &ctx->bn_arena, &ctx->bn_arena_cap, &ctx->err);
   if (rc == ZG_OK && n) {
     ctx->stats[8]++;
     if (batch_failed) ctx->stats[9]++;

@@ -23,6 +23,7 @@
 //   k_fe_*        lane per proof: final exponentiation in 5 launches (HBM workspace), f == 1 -> status
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -201,8 +202,8 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* inputs, 
                                                    PghrDec* dec, uint8_t* status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  bool ok = true;
-  for (int w = 0; w < 8; w++) ok = ok && okb[8 * (size_t)i + w];
+  bool ok = true;  // b's verdict (okb[8 i + 2]) joins in k_pghr_g2status: its decode runs concurrently
+  for (int w = 0; w < 8; w++) ok = ok && (w == 2 || okb[8 * (size_t)i + w]);
   if (!ok) {
     status[i] = ZG_STATUS_DECODE_INVALID;
     return;
@@ -235,6 +236,14 @@ __global__ void __launch_bounds__(64) k_pghr_prep(int n, const uint8_t* inputs, 
   o.pt[7] = aa;
   o.pt[8] = ba1_add(aa, c);  // acc + a + c
   status[i] = ZG_STATUS_OK;
+}
+
+// after k_pghr_decode_g2 (its own stream, concurrent with the G1 decodes, prep and rho): a proof
+// whose b failed to decode is DECODE_INVALID -- which precedes the input check, so it overrides
+// prep's INPUT_NONCANONICAL as well as OK (the reference's order)
+__global__ void __launch_bounds__(64) k_pghr_g2status(int n, const uint8_t* okb, uint8_t* status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !okb[8 * (size_t)i + 2]) status[i] = ZG_STATUS_DECODE_INVALID;
 }
 
 // the ten products rho_j Q of a proof, one per wave of a 640-lane block (64 proofs): wave w computes
@@ -399,41 +408,6 @@ __global__ void __launch_bounds__(64) k_pghr_bsum_final(int nb, const BJ1* part,
     }
   }
 }
-// lane per proof: the single-pair Miller loop e(P_i7, b_i) (the proof's own doubling / addition
-// steps), then the product of the block's 64 values in LDS -> part[block] (1 for proofs that are not OK)
-__global__ void __launch_bounds__(64) k_pghr_bmiller(int n, const PghrPts* pts, const uint8_t* status, Bq12* part) {
-  __shared__ Bq12 sh[64];
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  Bq12 f = b12_one();
-  if (i < n && status[i] == ZG_STATUS_OK && !pts[i].p[6].inf) {
-    const BA2 qb = pts[i].qb;
-    const BA1 p = pts[i].p[6];
-    BH2 t = {qb.x, qb.y, b2_one()};
-    for (int bit = ZG_BN_ATE_BITS - 2; bit >= -2; bit--) {
-      const int nsub = bit >= 0 ? (bn_ate_bit(bit) ? 2 : 1) : 1;
-      if (bit >= 0) f = b12_sqr(f);
-      for (int s = 0; s < nsub; s++) {
-        BLine l;
-        if (bit >= 0)
-          l = s == 0 ? bh2_dbl_step(&t) : bh2_add_step(&t, qb);
-        else if (bit == -1)
-          l = bh2_add_step(&t, ba2_frob(qb));
-        else {
-          const BA2 q2 = ba2_frob2(qb);
-          l = bh2_add_step(&t, {q2.x, b2_neg(q2.y)});
-        }
-        f = b12_mul_bline(f, l, p);
-      }
-    }
-  }
-  sh[threadIdx.x] = f;
-  __syncthreads();
-  for (int d = 32; d >= 1; d >>= 1) {
-    if ((int)threadIdx.x < d) sh[threadIdx.x] = b12_mul(sh[threadIdx.x], sh[threadIdx.x + d]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
-}
 // the six fixed pairs' Miller loop on the batch's sums, split by loop position (a lone lane carrying
 // all six took 39 ms, as long as the whole per-proof loop at 64k): lane (h, j) runs pair j over
 // segment h of the loop's 66 positions (bits 63..0 -- a doubling step and an addition when set --
@@ -479,12 +453,89 @@ __global__ void __launch_bounds__(64) k_pghr_fseg(const PghrPts* agg, const BLin
   __syncthreads();
   if (seg_lane && j == 0) seg[h] = b12_mul(b12_mul(sh[t], sh[t + 2]), sh[t + 4]);
 }
+#ifndef ZG_BSEG_WPE
+#define ZG_BSEG_WPE 1  // waves per SIMD the register budget allows (2 spills ~460 B/lane)
+#endif
+// grid (blocks of 64 lanes, ZG_PGHR_FSEG): lane g carries the proofs g, g + G, .., g + (K - 1) G
+// (G = ceil(n / K): a wave's line loads stay contiguous) over segment h = blockIdx.y as ONE
+// multi-pair loop -- a squaring shared by its K proofs per doubling step, then each proof's lines --
+// and the block multiplies its 64 values -> part[h gridDim.x + block] (1 where no proof is OK)
+__global__ void __launch_bounds__(64, ZG_BSEG_WPE) k_pghr_bseg(int n, int K, const PghrPts* pts, const uint8_t* status,
+                                                               const BLine* bl, Bq12* part) {
+  __shared__ Bq12 sh[64];
+  const int g = blockIdx.x * 64 + threadIdx.x, h = blockIdx.y, G = (n + K - 1) / K;
+  uint32_t live = 0;  // proof k of the lane takes part
+  for (int k = 0; k < K; k++) {
+    const int i = g + k * G;
+    if (g < G && i < n && status[i] == ZG_STATUS_OK && !pts[i].p[6].inf) live |= 1u << k;
+  }
+  Bq12 f = b12_one();
+  if (live) {
+    const int q0 = pghr_seg_lo(h), q1 = pghr_seg_lo(h + 1);
+    int li = 0;
+    for (int q = 0; q < q0; q++) {
+      const int bit = pghr_pos_bit(q);
+      li += bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
+    }
+    for (int q = q0; q < q1; q++) {
+      const int bit = pghr_pos_bit(q);
+      if (bit >= 0 && q > q0) f = b12_sqr(f);  // as k_pghr_fseg
+      const int nsub = bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
+      for (int s = 0; s < nsub; s++, li++)
+        for (int k = 0; k < K; k++) {
+          if (!((live >> k) & 1u)) continue;
+          const size_t i = (size_t)g + (size_t)k * G;
+          f = b12_mul_bline(f, bl[(size_t)li * n + i], pts[i].p[6]);
+        }
+    }
+  }
+  sh[threadIdx.x] = f;
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    if ((int)threadIdx.x < d) sh[threadIdx.x] = b12_mul(sh[threadIdx.x], sh[threadIdx.x + d]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)h * gridDim.x + blockIdx.x] = sh[0];
+}
+// seg[h] *= b[h stride] (the b pairs' segment products), seg[S] = 1 (k_fe_easy / k_pghr_fe_coop
+// keep their S + 1 inputs)
+__global__ void __launch_bounds__(64) k_pghr_segmul(Bq12* seg, const Bq12* b, size_t stride) {
+  const int h = threadIdx.x;
+  if (h < ZG_PGHR_FSEG) seg[h] = b12_mul(seg[h], b[stride * h]);
+  if (h == ZG_PGHR_FSEG) seg[h] = b12_one();
+}
 // one level of the product tree over the block products: dst[k] = src[2k] * src[2k + 1] (an odd
-// last one moves up)
-__global__ void __launch_bounds__(64) k_bn_tree(const Bq12* src, Bq12* dst, int m) {
+// last one moves up); blockIdx.y selects one of several independent trees (stride apart)
+__global__ void __launch_bounds__(64) k_bn_tree(const Bq12* src, Bq12* dst, int m, size_t stride) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (m + 1) / 2) return;
+  src += stride * blockIdx.y;
+  dst += stride * blockIdx.y;
   dst[k] = 2 * k + 1 < m ? b12_mul(src[2 * k], src[2 * k + 1]) : src[2 * k];
+}
+
+// The proofs' own pairs e(P_i7, b_i) of the batch check, split like the fixed pairs' loop (round 3;
+// one lane carrying a proof's whole single-pair loop left 64k proofs at one wave per SIMD, 11.6 ms):
+// k_pghr_blines walks each b_i's doubling / addition chain (lane per proof, G2 only) and stores its
+// 102 lines proof-minor (bl[li n + i], a wave's stores contiguous); k_pghr_bseg then runs lane
+// (proof, segment h) over that segment's lines from f = 1 -- eight times the waves -- and each block
+// multiplies its 64 values. Because the Horner product over segments is multiplicative,
+//   prod_i Horner(s_i0, .., s_i7) = Horner(prod_i s_i0, .., prod_i s_i7),
+// so the batch's b pairs join the fixed pairs segment by segment (k_pghr_segmul) and share their
+// Horner squarings and final exponentiation.
+__global__ void __launch_bounds__(64) k_pghr_blines(int n, const PghrPts* pts, const uint8_t* status, BLine* bl) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK || pts[i].p[6].inf) return;
+  const BA2 qb = pts[i].qb;
+  BH2 t = {qb.x, qb.y, b2_one()};
+  int li = 0;
+  for (int bit = ZG_BN_ATE_BITS - 2; bit >= 0; bit--) {
+    bl[(size_t)(li++) * n + i] = bh2_dbl_step(&t);
+    if (bn_ate_bit(bit)) bl[(size_t)(li++) * n + i] = bh2_add_step(&t, qb);
+  }
+  bl[(size_t)(li++) * n + i] = bh2_add_step(&t, ba2_frob(qb));
+  const BA2 q2 = ba2_frob2(qb);
+  bl[(size_t)li * n + i] = bh2_add_step(&t, {q2.x, b2_neg(q2.y)});
 }
 
 // the final exponentiation of zg_bn254.h bn_final_exp, split so that no kernel holds more than
@@ -770,6 +821,15 @@ void bn_dev_free(BnDev* d) {
   } while (0)
 
 static unsigned bn_blocks(long long n) { return (unsigned)((n + 63) / 64); }
+// k_pghr_bseg's proofs per lane (ZG_BSEG_K overrides): one up to 16k proofs (8 segments x 256
+// blocks = 2,048 waves), doubling while ceil(n / K) stays >= 16,384 lanes (64k proofs: 4), at most 8
+static int bseg_k(size_t n) {
+  static const int forced = getenv("ZG_BSEG_K") ? atoi(getenv("ZG_BSEG_K")) : 0;
+  if (forced > 0) return forced < 32 ? forced : 32;
+  int k = 1;
+  while (k < 8 && n / (size_t)(2 * k) >= 16384) k *= 2;
+  return k;
+}
 
 // hex strings of the key's JSON members in document order (crypto/src/json/pghr13.rs layout)
 static bool json_hex_list(const std::string& js, const char* key, std::vector<std::string>* out) {
@@ -899,94 +959,127 @@ int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, cons
   return ZG_OK;
 }
 
-int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* proofs, const uint8_t* inputs,
-                     const uint8_t* ninputs, const uint8_t* rho, uint8_t* status, float* kernel_ms,
-                     bool* batch_failed, std::string* err) {
+int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n, const uint8_t* proofs,
+                     const uint8_t* inputs, const uint8_t* ninputs, const uint8_t* rho, uint8_t* status,
+                     float* kernel_ms, bool* batch_failed, void** arena, size_t* arena_cap, std::string* err) {
   if (batch_failed) *batch_failed = false;
   if (!n) return ZG_OK;
-  // device buffers of this call
-  struct Bufs {
-    std::vector<void*> p;
-    ~Bufs() {
-      for (void* q : p) hipFree(q);
-    }
-  } bufs;
-  auto alloc = [&](void** x, size_t b) {
-    hipError_t e = hipMalloc(x, b ? b : 1);
-    if (e == hipSuccess) bufs.p.push_back(*x);
-    return e;
+  // the call's device buffers, carved from the context's grow-only arena (a 64k call needs
+  // ~1.5 GB; allocating and freeing that per call cost more wall time than most kernels)
+  const unsigned nb = bn_blocks(n);
+  struct Part {
+    void** p;
+    size_t b;
   };
-  uint8_t *dp, *din, *dni = nullptr, *drho, *dst;
-  PghrPts* dpts;
-  Bq12* df;
-  BCHK(alloc((void**)&dp, 296 * n));
-  BCHK(alloc((void**)&din, 9 * 32 * n));
-  BCHK(alloc((void**)&drho, ZG_PGHR_RHO_BYTES * n));
-  BCHK(alloc((void**)&dst, n));
-  BCHK(alloc((void**)&dpts, sizeof(PghrPts) * n));
+  uint8_t *dp, *din, *dni = nullptr, *drho, *dst, *dokb, *dbst;
+  PghrPts *dpts, *dagg;
   PghrDec* ddec;
   BA1* dmul;
-  BJ1* daccp;
-  uint8_t* dokb;
-  BCHK(alloc((void**)&ddec, sizeof(PghrDec) * n));
-  BCHK(alloc((void**)&dmul, sizeof(BA1) * ZG_PGHR_NMUL * n));
-  BCHK(alloc((void**)&daccp, sizeof(BJ1) * 9 * n));
-  BCHK(alloc((void**)&dokb, 8 * n));
-  BCHK(alloc((void**)&df, sizeof(Bq12) * 2 * n));
-  Bq12* dw;
-  BCHK(alloc((void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n));
+  BJ1 *daccp, *dpart;
+  BLine* dbl;
+  Bq12 *df, *dw, *dbseg, *dbtmp, *dseg, *dbw;
+  const Part parts[] = {
+      {(void**)&dp, 296 * n},
+      {(void**)&din, 9 * 32 * n},
+      {(void**)&drho, ZG_PGHR_RHO_BYTES * n},
+      {(void**)&dst, n},
+      {(void**)&dni, ninputs ? n : 0},
+      {(void**)&dpts, sizeof(PghrPts) * n},
+      {(void**)&ddec, sizeof(PghrDec) * n},
+      {(void**)&dmul, sizeof(BA1) * ZG_PGHR_NMUL * n},
+      {(void**)&daccp, sizeof(BJ1) * 9 * n},
+      {(void**)&dokb, 8 * n},
+      {(void**)&df, sizeof(Bq12) * 2 * n},
+      {(void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n},
+      {(void**)&dbl, sizeof(BLine) * ZG_BN_NLINES * n},
+      {(void**)&dpart, sizeof(BJ1) * ZG_BN_FIXED_Q * nb},
+      {(void**)&dagg, sizeof(PghrPts)},
+      {(void**)&dbseg, sizeof(Bq12) * ZG_PGHR_FSEG * nb},
+      {(void**)&dbtmp, sizeof(Bq12) * ZG_PGHR_FSEG * nb},
+      {(void**)&dseg, sizeof(Bq12) * (ZG_PGHR_FSEG + 1)},
+      {(void**)&dbw, sizeof(Bq12) * ZG_FE_SLOTS * (ZG_PGHR_FSEG + 1)},
+      {(void**)&dbst, ZG_PGHR_FSEG + 1},
+  };
+  size_t need = 0;
+  for (const Part& q : parts) need += (q.b + 255) & ~(size_t)255;
+  if (*arena_cap < need) {
+    BCHK(hipStreamSynchronize(st));
+    if (*arena) hipFree(*arena);
+    *arena = nullptr;
+    *arena_cap = 0;
+    BCHK(hipMalloc(arena, need));
+    *arena_cap = need;
+  }
+  char* bump = (char*)*arena;
+  for (const Part& q : parts) {
+    *q.p = q.b ? bump : nullptr;
+    bump += (q.b + 255) & ~(size_t)255;
+  }
+  struct Events {
+    hipEvent_t e[6] = {};
+    ~Events() {
+      for (hipEvent_t x : e)
+        if (x) hipEventDestroy(x);
+    }
+  } ev;
+  hipEvent_t &e0 = ev.e[0], &e1 = ev.e[1], &fork = ev.e[2], &join = ev.e[3], &g2fork = ev.e[4], &g2join = ev.e[5];
+  for (hipEvent_t* x : {&fork, &join, &g2fork, &g2join}) BCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
   BCHK(hipMemcpyAsync(dp, proofs, 296 * n, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(din, inputs, 9 * 32 * n, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(drho, rho, ZG_PGHR_RHO_BYTES * n, hipMemcpyHostToDevice, st));
-  if (ninputs) {
-    BCHK(alloc((void**)&dni, n));
-    BCHK(hipMemcpyAsync(dni, ninputs, n, hipMemcpyHostToDevice, st));
-  }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ninputs) BCHK(hipMemcpyAsync(dni, ninputs, n, hipMemcpyHostToDevice, st));
   if (kernel_ms) {
     BCHK(hipEventCreate(&e0));
     BCHK(hipEventCreate(&e1));
     BCHK(hipEventRecord(e0, st));
   }
-  hipLaunchKernelGGL(k_pghr_decode_g1, dim3(bn_blocks(n)), dim3(448), 0, st, (int)n, dp, ddec, dokb);
+  // b's decode (Fq2 sqrt + G2 membership, lane per proof at ~280 registers: one wave per SIMD)
+  // on the side stream, sharing the SIMDs with the G1 decodes, input combs, prep and rho
+  BCHK(hipEventRecord(g2fork, st));
+  BCHK(hipStreamWaitEvent(side, g2fork, 0));
+  hipLaunchKernelGGL(k_pghr_decode_g2, dim3(nb), dim3(64), 0, side, (int)n, dp, ddec, dokb);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_decode_g2, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dp, ddec, dokb);
+  BCHK(hipEventRecord(g2join, side));
+  hipLaunchKernelGGL(k_pghr_decode_g1, dim3(nb), dim3(448), 0, st, (int)n, dp, ddec, dokb);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_accp, dim3(bn_blocks(n)), dim3(576), 0, st, (int)n, din, dni, d->vk, d->comb, daccp);
+  hipLaunchKernelGGL(k_pghr_accp, dim3(nb), dim3(576), 0, st, (int)n, din, dni, d->vk, d->comb, daccp);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_prep, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, din, dni, d->vk, dokb, daccp, ddec,
-                     dst);
+  hipLaunchKernelGGL(k_pghr_prep, dim3(nb), dim3(64), 0, st, (int)n, din, dni, d->vk, dokb, daccp, ddec, dst);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_rho, dim3(bn_blocks(n)), dim3(64 * ZG_PGHR_NMUL), 0, st, (int)n, ddec, drho, dst, dmul);
+  hipLaunchKernelGGL(k_pghr_rho, dim3(nb), dim3(64 * ZG_PGHR_NMUL), 0, st, (int)n, ddec, drho, dst, dmul);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_combine, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
+  BCHK(hipStreamWaitEvent(st, g2join, 0));
+  hipLaunchKernelGGL(k_pghr_g2status, dim3(nb), dim3(64), 0, st, (int)n, dokb, dst);
+  hipLaunchKernelGGL(k_pghr_combine, dim3(nb), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
   BCHK(hipGetLastError());
-  // the batch check: six Miller loops on the sums, one single-pair loop per proof, one final exponentiation
-  const unsigned nb = bn_blocks(n);
-  BJ1* dpart;
-  PghrPts* dagg;
-  Bq12 *dbmil, *dbtmp, *dseg, *dbw;
-  uint8_t* dbst;
-  BCHK(alloc((void**)&dpart, sizeof(BJ1) * ZG_BN_FIXED_Q * nb));
-  BCHK(alloc((void**)&dagg, sizeof(PghrPts)));
-  BCHK(alloc((void**)&dbmil, sizeof(Bq12) * nb));
-  BCHK(alloc((void**)&dbtmp, sizeof(Bq12) * ((nb + 1) / 2)));
-  BCHK(alloc((void**)&dseg, sizeof(Bq12) * (ZG_PGHR_FSEG + 1)));
-  BCHK(alloc((void**)&dbw, sizeof(Bq12) * ZG_FE_SLOTS * (ZG_PGHR_FSEG + 1)));
-  BCHK(alloc((void**)&dbst, ZG_PGHR_FSEG + 1));
-  BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, st));
-  hipLaunchKernelGGL(k_pghr_bsum, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dpart);
-  hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, st, (int)nb, dpart, dagg);
-  hipLaunchKernelGGL(k_pghr_bmiller, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dbmil);
-  Bq12 *src = dbmil, *dstb = dbtmp;
-  for (int m = (int)nb; m > 1; m = (m + 1) / 2) {
-    hipLaunchKernelGGL(k_bn_tree, dim3(bn_blocks((m + 1) / 2)), dim3(64), 0, st, src, dstb, m);
+  // the batch check. Side stream: the six fixed pairs' operand sums and their loop by segments
+  // (single-wave kernels) -> dseg[0..S). Main stream, concurrently: the proofs' b lines, their
+  // segment values and one product tree per segment -> B_h; then dseg[h] *= B_h, the easy part of
+  // the S values, their Horner product and ONE hard part.
+  BCHK(hipEventRecord(fork, st));
+  BCHK(hipStreamWaitEvent(side, fork, 0));
+  BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, side));
+  hipLaunchKernelGGL(k_pghr_bsum, dim3(nb), dim3(64), 0, side, (int)n, dpts, dst, dpart);
+  hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, side, (int)nb, dpart, dagg);
+  hipLaunchKernelGGL(k_pghr_fseg, dim3(1), dim3(64), 0, side, dagg, d->lines, dseg);
+  BCHK(hipGetLastError());
+  BCHK(hipEventRecord(join, side));
+  hipLaunchKernelGGL(k_pghr_blines, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dbl);
+  // proofs per bseg lane: enough lanes for ~8 waves per SIMD... of the 1-wave-per-SIMD kernel, the
+  // rest as shared squarings (K proofs per squaring)
+  const int K = bseg_k(n);
+  const unsigned gb = bn_blocks(((long long)n + K - 1) / K);
+  hipLaunchKernelGGL(k_pghr_bseg, dim3(gb, ZG_PGHR_FSEG), dim3(64), 0, st, (int)n, K, dpts, dst, dbl, dbseg);
+  BCHK(hipGetLastError());
+  const size_t stride = gb;  // tree h over dbseg[h gb ..), dbtmp[h gb ..)
+  Bq12 *src = dbseg, *dstb = dbtmp;
+  for (int m = (int)gb; m > 1; m = (m + 1) / 2) {
+    hipLaunchKernelGGL(k_bn_tree, dim3(bn_blocks((m + 1) / 2), ZG_PGHR_FSEG), dim3(64), 0, st, src, dstb, m, stride);
     std::swap(src, dstb);
   }
-  BCHK(hipMemcpyAsync(dseg + ZG_PGHR_FSEG, src, sizeof(Bq12), hipMemcpyDeviceToDevice, st));
-  // the fixed pairs' loop on the sums by segments -> dseg[0..S); the easy part of all S + 1 values,
-  // their Horner product, the hard part of that one value
-  hipLaunchKernelGGL(k_pghr_fseg, dim3(1), dim3(64), 0, st, dagg, d->lines, dseg);
+  BCHK(hipGetLastError());
+  BCHK(hipStreamWaitEvent(st, join, 0));
+  hipLaunchKernelGGL(k_pghr_segmul, dim3(1), dim3(64), 0, st, dseg, src, stride);
   hipLaunchKernelGGL(k_fe_easy, dim3(1), dim3(64), 0, st, ZG_PGHR_FSEG + 1, dseg, dbst, dbw, 1);
   hipLaunchKernelGGL(k_pghr_fe_coop, dim3(1), dim3(64), 0, st, dbw, dbst);
   BCHK(hipGetLastError());
@@ -996,28 +1089,23 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, size_t n, const uint8_t* pr
   if (batch_failed) *batch_failed = bok != ZG_STATUS_OK;
   if (bok != ZG_STATUS_OK) {  // some proof fails: the per-proof path for the exact statuses
     const int halves = n < ZG_PGHR_SPLIT_BELOW ? 2 : 1;
-    hipLaunchKernelGGL(k_pghr_miller, dim3(bn_blocks(n)), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df,
-                       halves);
+    hipLaunchKernelGGL(k_pghr_miller, dim3(nb), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df, halves);
     BCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_easy, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, df, dst, dw, halves);
+    hipLaunchKernelGGL(k_fe_easy, dim3(nb), dim3(64), 0, st, (int)n, df, dst, dw, halves);
     BCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_exp<1>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    hipLaunchKernelGGL(k_fe_exp<1>, dim3(nb), dim3(64), 0, st, (int)n, dst, dw);
     BCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_exp<2>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    hipLaunchKernelGGL(k_fe_exp<2>, dim3(nb), dim3(64), 0, st, (int)n, dst, dw);
     BCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_exp<3>, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    hipLaunchKernelGGL(k_fe_exp<3>, dim3(nb), dim3(64), 0, st, (int)n, dst, dw);
     BCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_fe_last, dim3(bn_blocks(n)), dim3(64), 0, st, (int)n, dst, dw);
+    hipLaunchKernelGGL(k_fe_last, dim3(nb), dim3(64), 0, st, (int)n, dst, dw);
     BCHK(hipGetLastError());
   }
   if (kernel_ms) BCHK(hipEventRecord(e1, st));
   BCHK(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, st));
   BCHK(hipStreamSynchronize(st));
-  if (kernel_ms) {
-    BCHK(hipEventElapsedTime(kernel_ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-  }
+  if (kernel_ms) BCHK(hipEventElapsedTime(kernel_ms, e0, e1));
   return ZG_OK;
 }
 

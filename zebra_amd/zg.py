@@ -355,18 +355,24 @@ class Context:
 
     def pghr13_verify(self, proofs, inputs, n_inputs=None, with_time=False):
         """proofs: 296-byte PHGR proofs; inputs: per proof a list of <= 9 32-byte LE BN254 Fr
-        (Input::into_bn_frs) -> statuses (STATUS_*)"""
-        n = len(proofs)
-        rows = []
-        for r in inputs:
-            r = [bytes(x) for x in r]
-            assert len(r) <= 9
-            rows.append(b"".join(r) + bytes(32 * (9 - len(r))))
-        cnt = bytes(len(r) for r in inputs) if n_inputs is None else bytes(n_inputs)
+        (Input::into_bn_frs) -> statuses (STATUS_*). Packed form (the ABI's own buffers): proofs a
+        bytes of n * 296, inputs a bytes of n * 288 (9 slots of 32 per proof) and n_inputs given."""
+        if isinstance(proofs, (bytes, bytearray)):
+            n = len(proofs) // 296
+            assert len(proofs) == 296 * n and len(inputs) == 288 * n and n_inputs is not None and len(n_inputs) == n
+            pblob, iblob, cnt = proofs, inputs, bytes(n_inputs)
+        else:
+            n = len(proofs)
+            rows = []
+            for r in inputs:
+                r = [bytes(x) for x in r]
+                assert len(r) <= 9
+                rows.append(b"".join(r) + bytes(32 * (9 - len(r))))
+            cnt = bytes(len(r) for r in inputs) if n_inputs is None else bytes(n_inputs)
+            pblob, iblob = b"".join(map(bytes, proofs)), b"".join(rows)
         st = ctypes.create_string_buffer(max(n, 1))
         ms = ctypes.c_float(0)
-        self._chk(lib().zg_pghr13_verify(self._p, n, b"".join(map(bytes, proofs)), b"".join(rows), cnt, st,
-                                         ctypes.byref(ms)))
+        self._chk(lib().zg_pghr13_verify(self._p, n, pblob, iblob, cnt, st, ctypes.byref(ms)))
         out = list(st.raw[:n])
         return (out, ms.value) if with_time else out
 
