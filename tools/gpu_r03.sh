@@ -61,7 +61,7 @@ for s in $STEPS; do
       echo "$v $(cat $O/pghr_${v}_$n.json)"
     done; done ;;
   pghrk)
-    for v in main $VARIANTS; do for k in 1 2 4 8; do
+    for v in main $VARIANTS; do for k in ${KS:-1 2 4 8}; do
       lv=$v; [ $v = main ] && lv=
       ZG_LIB_VARIANT=$lv ZG_BSEG_K=$k timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n 65536 > $O/pghrk_${v}_$k.json 2> $O/pghrk_${v}_$k.err || { echo "pghr bench $v $k failed"; tail -30 $O/pghrk_${v}_$k.err; exit 1; }
       echo "$v K=$k $(cat $O/pghrk_${v}_$k.json)"

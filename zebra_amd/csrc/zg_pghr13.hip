@@ -3,7 +3,7 @@
 //
 // Reference: crypto/src/pghr13.rs:69-105 (Proof::from_raw, verify), called per PHGR JoinSplit by
 // verification/src/sprout.rs:61-67. verify checks five pairing equalities; here, per proof, the five
-// are folded into one product with random 128-bit weights rho_2..rho_5 (rho_1 = 1):
+// are folded into one product with random 128-bit weights rho_1..rho_5:
 //
 //   e(a, A) e(P1', P2) e(rho3 c, C) e(rho4 k, G) e(P5, GB2) e(P6, Z) e(P7, b) == 1
 //   P1' = -(rho1 a' + rho2 b' + rho3 c' + rho5 c)     P5 = -rho4 (acc + a + c)     P6 = -rho5 h
@@ -11,16 +11,20 @@
 //   P7  = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a)
 //
 // which holds for all rho iff each equality holds (a false proof passes with probability
-// ~2^-128 over the rho, drawn from getrandom(2) per call). One multi-Miller loop over 7 pairs and
-// one final exponentiation per proof, instead of 10 pairings: the 6 verifying-key G2 points use
-// line tables built once per device, only the proof's b is doubled along the loop.
+// ~2^-128 over the rho, drawn from getrandom(2) per call). A call is decided by ONE check: the six
+// key pairs on the batch's operand sums, the proofs' own b pairs, one final exponentiation; only a
+// failing call runs the per-proof path (one 7-pair multi-Miller loop + final exponentiation each).
 //
-//   k_bn_vk       VK points -> Montgomery, AffineG1/G2::new checks (curve, G2 order r)
-//   k_bn_lines    line coefficients of the 6 fixed G2 points (lane per point)
-//   k_bn_comb     byte-window comb tables of the fixed G1 bases (ic[0..9], vk.b, gammaBeta1)
-//   k_pghr_prep   lane per proof: decode, acc = ic0 + sum x_i ic_{i+1}, the 7 G1 operands
-//   k_pghr_miller lane per proof: the multi-Miller loop -> f (HBM)
-//   k_fe_*        lane per proof: final exponentiation in 5 launches (HBM workspace), f == 1 -> status
+//   key (once per device): k_bn_vk (points, AffineG1/G2::new checks), k_bn_lines (the 6 fixed G2
+//     points' lines), k_bn_comb (byte-window combs of ic[], vk.b, gammaBeta1)
+//   main stream: k_pghr_decode_g1 (wave per point), k_pghr_accp (input combs), k_pghr_prep
+//     (statuses, acc), k_pghr_rho (the weighted products, GLV), then k_pghr_g2status, k_pghr_combine
+//     (the 7 G1 operands), k_pghr_bseg (the b pairs by loop segment), k_bn_tree (per-segment
+//     products), k_pghr_segmul, k_fe_easy, k_pghr_fe_coop (one wave)
+//   side stream: k_pghr_decode_g2 (Fq2 sqrt + G2 membership) and k_pghr_blines (b's lines -> HBM),
+//     concurrent with the G1 chain; then k_pghr_bsum(_final) and k_pghr_fseg (the key pairs on the
+//     batch's operand sums, by segment), concurrent with k_pghr_bseg
+//   per-proof path: k_pghr_miller, k_fe_easy, k_fe_exp<1..3>, k_fe_last
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -459,7 +463,12 @@ __global__ void __launch_bounds__(64) k_pghr_fseg(const PghrPts* agg, const BLin
 // grid (blocks of 64 lanes, ZG_PGHR_FSEG): lane g carries the proofs g, g + G, .., g + (K - 1) G
 // (G = ceil(n / K): a wave's line loads stay contiguous) over segment h = blockIdx.y as ONE
 // multi-pair loop -- a squaring shared by its K proofs per doubling step, then each proof's lines --
-// and the block multiplies its 64 values -> part[h gridDim.x + block] (1 where no proof is OK)
+// and the block multiplies its 64 values -> part[h gridDim.x + block] (1 where no proof is OK).
+// The Horner product over segments is multiplicative,
+//   prod_i Horner(s_i0, .., s_i7) = Horner(prod_i s_i0, .., prod_i s_i7),
+// so the b pairs join the key pairs segment by segment (k_pghr_segmul) and share their Horner
+// squarings and final exponentiation. (The key pairs as lanes of this grid instead, after their
+// operand sums on this stream: 64k 31.7 -> 33.1 ms, 8k 14.6 -> 16.3, profiles/r03y_pghr13_bench.txt.)
 __global__ void __launch_bounds__(64, ZG_BSEG_WPE) k_pghr_bseg(int n, int K, const PghrPts* pts, const uint8_t* status,
                                                                const BLine* bl, Bq12* part) {
   __shared__ Bq12 sh[64];
@@ -514,19 +523,16 @@ __global__ void __launch_bounds__(64) k_bn_tree(const Bq12* src, Bq12* dst, int 
   dst[k] = 2 * k + 1 < m ? b12_mul(src[2 * k], src[2 * k + 1]) : src[2 * k];
 }
 
-// The proofs' own pairs e(P_i7, b_i) of the batch check, split like the fixed pairs' loop (round 3;
-// one lane carrying a proof's whole single-pair loop left 64k proofs at one wave per SIMD, 11.6 ms):
-// k_pghr_blines walks each b_i's doubling / addition chain (lane per proof, G2 only) and stores its
-// 102 lines proof-minor (bl[li n + i], a wave's stores contiguous); k_pghr_bseg then runs lane
-// (proof, segment h) over that segment's lines from f = 1 -- eight times the waves -- and each block
-// multiplies its 64 values. Because the Horner product over segments is multiplicative,
-//   prod_i Horner(s_i0, .., s_i7) = Horner(prod_i s_i0, .., prod_i s_i7),
-// so the batch's b pairs join the fixed pairs segment by segment (k_pghr_segmul) and share their
-// Horner squarings and final exponentiation.
-__global__ void __launch_bounds__(64) k_pghr_blines(int n, const PghrPts* pts, const uint8_t* status, BLine* bl) {
+// The proofs' own pairs e(P_i7, b_i) of the batch check go by segment too (one lane carrying a
+// proof's whole single-pair loop left 64k proofs at one wave per SIMD, 11.6 ms): k_pghr_blines walks
+// each b_i's doubling / addition chain (lane per proof, G2 only) and stores its 102 lines
+// proof-minor (bl[li n + i], a wave's stores contiguous) for k_pghr_bseg. It needs only the decoded
+// b, so it follows k_pghr_decode_g2 on the side stream, concurrent with the G1 chain (decode, combs,
+// prep, rho); a proof that fails elsewhere leaves its lines unread.
+__global__ void __launch_bounds__(64) k_pghr_blines(int n, const PghrDec* dec, const uint8_t* okb, BLine* bl) {
   const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n || status[i] != ZG_STATUS_OK || pts[i].p[6].inf) return;
-  const BA2 qb = pts[i].qb;
+  if (i >= n || !okb[8 * (size_t)i + 2]) return;
+  const BA2 qb = dec[i].qb;
   BH2 t = {qb.x, qb.y, b2_one()};
   int li = 0;
   for (int bit = ZG_BN_ATE_BITS - 2; bit >= 0; bit--) {
@@ -821,13 +827,14 @@ void bn_dev_free(BnDev* d) {
   } while (0)
 
 static unsigned bn_blocks(long long n) { return (unsigned)((n + 63) / 64); }
-// k_pghr_bseg's proofs per lane (ZG_BSEG_K overrides): one up to 16k proofs (8 segments x 256
-// blocks = 2,048 waves), doubling while ceil(n / K) stays >= 16,384 lanes (64k proofs: 4), at most 8
+// k_pghr_bseg's proofs per lane (ZG_BSEG_K overrides): ceil(n / K) >= 8,192 lanes x 8 segments
+// (1,024 waves of the one-wave-per-SIMD kernel), the rest as shared squarings: 64k proofs K = 8
+// (kernels 39.0 / 36.0 / 34.6 / 32.9 ms for K = 1 / 2 / 4 / 8, profiles/r03v_pghr13_bench.txt)
 static int bseg_k(size_t n) {
   static const int forced = getenv("ZG_BSEG_K") ? atoi(getenv("ZG_BSEG_K")) : 0;
   if (forced > 0) return forced < 32 ? forced : 32;
   int k = 1;
-  while (k < 8 && n / (size_t)(2 * k) >= 16384) k *= 2;
+  while (k < 8 && n / (size_t)(2 * k) >= 8192) k *= 2;
   return k;
 }
 
@@ -1033,11 +1040,12 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
     BCHK(hipEventCreate(&e1));
     BCHK(hipEventRecord(e0, st));
   }
-  // b's decode (Fq2 sqrt + G2 membership, lane per proof at ~280 registers: one wave per SIMD)
-  // on the side stream, sharing the SIMDs with the G1 decodes, input combs, prep and rho
+  // b's decode (Fq2 sqrt + G2 membership) and its lines (lane per proof at ~280 registers: one
+  // wave per SIMD) on the side stream, sharing the SIMDs with the G1 decodes, combs, prep and rho
   BCHK(hipEventRecord(g2fork, st));
   BCHK(hipStreamWaitEvent(side, g2fork, 0));
   hipLaunchKernelGGL(k_pghr_decode_g2, dim3(nb), dim3(64), 0, side, (int)n, dp, ddec, dokb);
+  hipLaunchKernelGGL(k_pghr_blines, dim3(nb), dim3(64), 0, side, (int)n, ddec, dokb, dbl);
   BCHK(hipGetLastError());
   BCHK(hipEventRecord(g2join, side));
   hipLaunchKernelGGL(k_pghr_decode_g1, dim3(nb), dim3(448), 0, st, (int)n, dp, ddec, dokb);
@@ -1053,9 +1061,9 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   hipLaunchKernelGGL(k_pghr_combine, dim3(nb), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
   BCHK(hipGetLastError());
   // the batch check. Side stream: the six fixed pairs' operand sums and their loop by segments
-  // (single-wave kernels) -> dseg[0..S). Main stream, concurrently: the proofs' b lines, their
-  // segment values and one product tree per segment -> B_h; then dseg[h] *= B_h, the easy part of
-  // the S values, their Horner product and ONE hard part.
+  // (single-wave kernels) -> dseg[0..S). Main stream, concurrently: the b pairs' segment values
+  // (from k_pghr_blines' lines) and one product tree per segment -> B_h; then dseg[h] *= B_h, the
+  // easy part of the S values, their Horner product and ONE hard part.
   BCHK(hipEventRecord(fork, st));
   BCHK(hipStreamWaitEvent(side, fork, 0));
   BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, side));
@@ -1064,7 +1072,6 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   hipLaunchKernelGGL(k_pghr_fseg, dim3(1), dim3(64), 0, side, dagg, d->lines, dseg);
   BCHK(hipGetLastError());
   BCHK(hipEventRecord(join, side));
-  hipLaunchKernelGGL(k_pghr_blines, dim3(nb), dim3(64), 0, st, (int)n, dpts, dst, dbl);
   // proofs per bseg lane: enough lanes for ~8 waves per SIMD... of the 1-wave-per-SIMD kernel, the
   // rest as shared squarings (K proofs per squaring)
   const int K = bseg_k(n);
