@@ -54,7 +54,7 @@ for s in $STEPS; do
     done
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pghr -o run -- python3 $R/tools/bench_pghr13.py --no-cpu --reps 2 > /dev/null 2> $O/prof_pghr.err || { echo "rocprof pghr failed"; tail -30 $O/prof_pghr.err; exit 1; }
-    cd $R && python3 tools/rocpd_stats.py $O/prof_pghr/run_results.db $O/kernel_stats_pghr.csv && rm -f $O/prof_pghr/run_results.db ;;
+    cd $R && python3 tools/rocpd_stats.py $O/prof_pghr/run_results.db $O/kernel_stats_pghr.csv && python3 tools/timeline.py $O/prof_pghr/run_results.db k_pghr_decode_g1 $O/pghr_timeline.txt > /dev/null && rm -f $O/prof_pghr/run_results.db ;;
   pghrvar)
     for v in $VARIANTS; do for n in 65536 8192; do
       ZG_LIB_VARIANT=$v timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n $n > $O/pghr_${v}_$n.json 2> $O/pghr_${v}_$n.err || { echo "pghr bench $v failed"; tail -30 $O/pghr_${v}_$n.err; exit 1; }
@@ -65,6 +65,11 @@ for s in $STEPS; do
       lv=$v; [ $v = main ] && lv=
       ZG_LIB_VARIANT=$lv ZG_BSEG_K=$k timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n 65536 > $O/pghrk_${v}_$k.json 2> $O/pghrk_${v}_$k.err || { echo "pghr bench $v $k failed"; tail -30 $O/pghrk_${v}_$k.err; exit 1; }
       echo "$v K=$k $(cat $O/pghrk_${v}_$k.json)"
+    done; done ;;
+  pghrb)
+    for b in 1 2 4; do for n in 65536 8192; do
+      ZG_STRAUS_B=$b timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n $n > $O/pghrb_${b}_$n.json 2> $O/pghrb_${b}_$n.err || { echo "pghr bench B=$b failed"; tail -30 $O/pghrb_${b}_$n.err; exit 1; }
+      echo "B=$b $(cat $O/pghrb_${b}_$n.json)"
     done; done ;;
   pghrtests)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_pghr13.py tests/test_collector.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_pghr.log 2>&1 || { echo "gpu pghr tests failed"; tail -60 $O/gpu_tests_pghr.log; exit 1; }

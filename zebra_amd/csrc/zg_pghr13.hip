@@ -18,13 +18,14 @@
 //   key (once per device): k_bn_vk (points, AffineG1/G2::new checks), k_bn_lines (the 6 fixed G2
 //     points' lines), k_bn_comb (byte-window combs of ic[], vk.b, gammaBeta1)
 //   main stream: k_pghr_decode_g1 (wave per point), k_pghr_accp (input combs), k_pghr_prep
-//     (statuses, acc), k_pghr_rho (the weighted products, GLV), then k_pghr_g2status, k_pghr_combine
-//     (the 7 G1 operands), k_pghr_bseg (the b pairs by loop segment), k_bn_tree (per-segment
-//     products), k_pghr_segmul, k_fe_easy, k_pghr_fe_coop (one wave)
-//   side stream: k_pghr_decode_g2 (Fq2 sqrt + G2 membership) and k_pghr_blines (b's lines -> HBM),
-//     concurrent with the G1 chain; then k_pghr_bsum(_final) and k_pghr_fseg (the key pairs on the
-//     batch's operand sums, by segment), concurrent with k_pghr_bseg
-//   per-proof path: k_pghr_miller, k_fe_easy, k_fe_exp<1..3>, k_fe_last
+//     (statuses, acc), k_pghr_g2status, k_pghr_straus (the key pairs' operand sums, Straus over the
+//     GLV halves), k_pghr_ssum / k_pghr_bsum_final, k_pghr_bseg
+//     (every pair of the batch by loop segment), k_bn_tree (per-segment products), k_pghr_segcopy,
+//     k_fe_easy, k_pghr_fe_coop (one wave)
+//   side stream: k_pghr_decode_g2 (Fq2 sqrt + G2 membership), k_pghr_blines (b's lines -> HBM) and
+//     k_pghr_p7 (the b pairs' operands), concurrent with the G1 chain and the Straus sums
+//   per-proof path (a failing batch): k_pghr_rho + k_pghr_combine (every P_i), k_pghr_miller,
+//     k_fe_easy, k_fe_exp<1..3>, k_fe_last
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -160,15 +161,15 @@ struct PghrDec {
   BA2 qb;
 };
 
-// Proof::from_raw's point decodes: the seven G1 points one per wave of a 448-lane block (64 proofs;
+// Proof::from_raw's point decodes: the seven G1 points one per one-wave block (grid y; 64 proofs;
 // bytes a 0, a' 33, b' 131, c 164, c' 197, k 230, h 263) and the G2 point b (bytes 66..130: the
 // Fq2 square root and the G2 membership test, far heavier) in a launch of its own, lane per proof,
 // so the light waves do not hold a block open behind it -> dec, verdicts -> okb[8 i + w] (w = 2: b).
 __device__ __constant__ const int16_t PGHR_DEC_OFF[7] = {0, 33, 131, 164, 197, 230, 263};
 __device__ __constant__ const int8_t PGHR_DEC_OK[7] = {0, 1, 3, 4, 5, 6, 7};
-__global__ void __launch_bounds__(448) k_pghr_decode_g1(int n, const uint8_t* proofs, PghrDec* dec, uint8_t* okb) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;  // wave-uniform: slot w of dec.pt
+__global__ void __launch_bounds__(64) k_pghr_decode_g1(int n, const uint8_t* proofs, PghrDec* dec, uint8_t* okb) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int w = blockIdx.y;  // slot w of dec.pt
   if (i >= n) return;
   BA1 a;
   const bool ok = bn_g1_decode(proofs + (size_t)296 * i + PGHR_DEC_OFF[w], &a);
@@ -184,13 +185,13 @@ __global__ void __launch_bounds__(64) k_pghr_decode_g2(int n, const uint8_t* pro
   okb[8 * (size_t)i + 2] = ok;
 }
 
-// x_j ic_{j+1} for the nine input slots, one per wave of a 576-lane block (byte-window combs, 32
+// x_j ic_{j+1} for the nine input slots, one per one-wave block (grid y; byte-window combs, 32
 // mixed additions each) -> accp[9 i + j] (infinity past the proof's input count); canonicity is
 // k_pghr_prep's
-__global__ void __launch_bounds__(576) k_pghr_accp(int n, const uint8_t* inputs, const uint8_t* ninputs,
-                                                    const BnVK* vk, const uint32_t* comb, BJ1* accp) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = threadIdx.x >> 6;  // wave-uniform
+__global__ void __launch_bounds__(64) k_pghr_accp(int n, const uint8_t* inputs, const uint8_t* ninputs,
+                                                   const BnVK* vk, const uint32_t* comb, BJ1* accp) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int j = blockIdx.y;
   if (i >= n) return;
   int cnt = ninputs ? ninputs[i] : 9;
   cnt = cnt < vk->ic_len - 1 ? cnt : vk->ic_len - 1;
@@ -315,6 +316,116 @@ __global__ void __launch_bounds__(64) k_pghr_combine(int n, const PghrDec* dec, 
   o.qb = d.qb;
 }
 
+// ---- the batch path's G1 operands without the nine per-proof products that only feed sums.
+// Of the ten weighted products of a proof, nine enter the batch check only through the six key pairs'
+// operand sums S_j = sum_i P_ij (the per-proof path's P_i0..P_i5), so k_pghr_straus forms those sums directly: lane
+// (family f, group g) carries the B proofs g, g + G, .. (G = ceil(n / B)) and computes
+// sum_k [a_k + b_k lambda] q_k as ONE joint double-and-add -- 64 doublings shared by its B proofs,
+// each adding q, phi(q) or q + phi(q) by its two bits (Straus' interleaving over the GLV halves)
+// instead of 64 doublings per product. Only the b pair's operand P_i7 (one product per proof,
+// k_pghr_p7) stays per proof; a failing batch's per-proof path forms every P_i (k_pghr_rho, combine).
+// family: (point, weight, sum, negated): the PGHR_RHO_MUL rows but {7, 3} (P7's)
+#define ZG_PGHR_NFAM 9
+__device__ __constant__ const int8_t PGHR_FAM[ZG_PGHR_NFAM][4] = {
+    {2, 0, 1, 1},  // rho2 b'           -> -S1
+    {4, 1, 1, 1},  // rho3 c'           -> -S1
+    {3, 3, 1, 1},  // rho5 c            -> -S1
+    {1, 4, 1, 1},  // rho1 a'           -> -S1
+    {3, 1, 2, 0},  // rho3 c            ->  S2
+    {5, 2, 3, 0},  // rho4 k            ->  S3
+    {8, 2, 4, 1},  // rho4 (acc + a + c) -> -S4
+    {6, 3, 5, 1},  // rho5 h            -> -S5
+    {0, 4, 0, 0},  // rho1 a            ->  S0
+};
+ZG_INL void pghr_rho_words(const uint8_t* r, uint32_t* rw) {
+  for (int l = 0; l < 4; l++)
+    rw[l] = (uint32_t)r[4 * l] | ((uint32_t)r[4 * l + 1] << 8) | ((uint32_t)r[4 * l + 2] << 16) |
+            ((uint32_t)r[4 * l + 3] << 24);
+}
+// grid (ceil(G / 64), families) -> part[f G + g] (Jacobian; infinity where no proof of the lane is OK)
+template <int B>
+__global__ void __launch_bounds__(64) k_pghr_straus(int n, const PghrDec* dec, const uint8_t* rho,
+                                                     const uint8_t* status, BJ1* part) {
+  const int g = blockIdx.x * 64 + threadIdx.x, f = blockIdx.y, G = (n + B - 1) / B;
+  if (g >= G) return;
+  const int pj = PGHR_FAM[f][0], rj = PGHR_FAM[f][1];
+  BA1 q[B], s[B];
+  uint32_t rw[B][4];
+#pragma unroll
+  for (int k = 0; k < B; k++) {
+    const int i = g + k * G;
+    q[k] = {bq_zero(), bq_zero(), true};
+    if (i < n && status[i] == ZG_STATUS_OK) q[k] = dec[i].pt[pj];
+    pghr_rho_words(rho + (size_t)ZG_PGHR_RHO_BYTES * (q[k].inf ? 0 : i) + 16 * rj, rw[k]);
+    s[k] = q[k].inf ? q[k] : ba1_add(q[k], ba1_phi(q[k]));  // != O: phi(q) = -q would need lambda = -1
+  }
+  BJ1 acc = bj1_inf();
+  for (int b = 63; b >= 0; b--) {
+    acc = bj1_dbl(acc);
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      if (q[k].inf) continue;
+      const uint32_t ba = (rw[k][b >> 5] >> (b & 31)) & 1u, bb = (rw[k][2 + (b >> 5)] >> (b & 31)) & 1u;
+      if (ba | bb) acc = bj1_add_aff(acc, ba & bb ? s[k] : ba ? q[k] : ba1_phi(q[k]));
+    }
+  }
+  part[(size_t)f * G + g] = acc;
+}
+// sum j's entries are the G partials of each of its families; block (j, c) adds entries
+// [c CH, (c + 1) CH) of that list (64 lanes strided, then an LDS tree), negated for the negated sums
+// -> part1[c * 6 + j] (infinity past the list): k_pghr_bsum_final's input layout
+#define ZG_PGHR_SSUM_CH 1024
+__global__ void __launch_bounds__(64) k_pghr_ssum(int G, const BJ1* part, BJ1* part1) {
+  __shared__ BJ1 sh[64];
+  const int j = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  int fam[4], nf = 0;
+  bool neg = false;
+  for (int f = 0; f < ZG_PGHR_NFAM; f++)
+    if (PGHR_FAM[f][2] == j) {
+      fam[nf++] = f;
+      neg = PGHR_FAM[f][3];
+    }
+  const long long len = (long long)nf * G, e0 = (long long)c * ZG_PGHR_SSUM_CH;
+  BJ1 acc = bj1_inf();
+  for (long long e = e0 + t; e < e0 + ZG_PGHR_SSUM_CH && e < len; e += 64)
+    acc = bj1_add(acc, part[(size_t)fam[e / G] * G + (size_t)(e % G)]);
+  sh[t] = acc;
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    if (t < d) sh[t] = bj1_add(sh[t], sh[t + d]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    BJ1 r = sh[0];
+    if (neg) r.Y = bq_neg(r.Y);
+    part1[(size_t)c * ZG_BN_FIXED_Q + j] = r;
+  }
+}
+// lane per proof: P_i7 = rho2 vk.b - rho4 gammaBeta1 + rho5 (acc + a) (k_pghr_combine's, with the
+// one variable-base product here) and b -> pts[i].p[6], pts[i].qb
+__global__ void __launch_bounds__(64) k_pghr_p7(int n, const PghrDec* dec, const uint8_t* rho, const uint32_t* comb,
+                                                 const uint8_t* status, PghrPts* pts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != ZG_STATUS_OK) return;
+  const PghrDec& d = dec[i];
+  const uint8_t* r = rho + (size_t)ZG_PGHR_RHO_BYTES * i;
+  uint32_t rw[4];
+  pghr_rho_words(r + 16 * 3, rw);  // rho5
+  BJ1 t = bn_comb_mul(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC, r, 8), comb, ZG_BN_MAX_IC, r + 8, 8, true);
+  const BA1 g4 = bj1_to_aff(
+      bn_comb_mul(bn_comb_mul(bj1_inf(), comb, ZG_BN_MAX_IC + 1, r + 32, 8), comb, ZG_BN_MAX_IC + 1, r + 40, 8, true));
+  t = bj1_add_aff(t, ba1_neg(g4));
+  if (!d.pt[7].inf) t = bj1_add(t, bj1_mul_glv(d.pt[7], rw));
+  pts[i].p[6] = bj1_to_aff(t);
+  pts[i].qb = d.qb;
+}
+// B by size: enough (family, group) lanes for ~2 waves per SIMD, the rest as shared doublings
+static int straus_b(size_t n) {
+  static const int forced = getenv("ZG_STRAUS_B") ? atoi(getenv("ZG_STRAUS_B")) : 0;
+  if (forced == 1 || forced == 2 || forced == 4) return forced;
+  return n >= 57344 ? 4 : n >= 28672 ? 2 : 1;
+}
+
 // the multi-Miller loop of one proof's 7 pairs, split over two waves of a 128-lane block (the same
 // 64 proofs): wave 0 carries pairs 0..3 (fixed G2 points), wave 1 pairs 4, 5 and the proof's own b
 // (its doubling / addition steps), each with its own accumulator (one extra Fq12 squaring per step),
@@ -375,23 +486,8 @@ __global__ void __launch_bounds__(128) k_pghr_miller(int n, const PghrPts* pts, 
 // it equals 1 iff every proof's five equalities hold, but for a probability <= 2^-128 per false
 // one (each equality of each proof carries its own independent 128-bit weight). A batch that fails
 // re-runs the per-proof path (k_pghr_miller + k_fe_*) for the exact statuses.
-// per block (64 proofs): the sums of the six fixed-Q operands over the proofs whose status is OK
-__global__ void __launch_bounds__(64) k_pghr_bsum(int n, const PghrPts* pts, const uint8_t* status, BJ1* part) {
-  __shared__ BJ1 sh[64];
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  const bool live = i < n && status[i] == ZG_STATUS_OK;
-  for (int j = 0; j < ZG_BN_FIXED_Q; j++) {
-    sh[threadIdx.x] = live ? bj1_from(pts[i].p[j]) : bj1_inf();
-    __syncthreads();
-    for (int d = 32; d >= 1; d >>= 1) {
-      if ((int)threadIdx.x < d) sh[threadIdx.x] = bj1_add(sh[threadIdx.x], sh[threadIdx.x + d]);
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) part[(size_t)blockIdx.x * ZG_BN_FIXED_Q + j] = sh[0];
-    __syncthreads();
-  }
-}
-// block j of six: sum_i P_ij over the nb block partials (lanes stride, then an LDS tree) -> agg->p[j];
+// block j of six: sum_i P_ij over the nb chunk partials of k_pghr_ssum (lanes stride, then an LDS
+// tree) -> agg->p[j];
 // agg->p[6] = infinity (the aggregate has no b pair)
 __global__ void __launch_bounds__(64) k_pghr_bsum_final(int nb, const BJ1* part, PghrPts* agg) {
   __shared__ BJ1 sh[64];
@@ -412,18 +508,16 @@ __global__ void __launch_bounds__(64) k_pghr_bsum_final(int nb, const BJ1* part,
     }
   }
 }
-// the six fixed pairs' Miller loop on the batch's sums, split by loop position (a lone lane carrying
-// all six took 39 ms, as long as the whole per-proof loop at 64k): lane (h, j) runs pair j over
-// segment h of the loop's 66 positions (bits 63..0 -- a doubling step and an addition when set --
-// then the pi(Q), -pi^2(Q) additions) from f = 1, and the block multiplies each segment's six pair
-// values in LDS -> seg[h]. The loop's value is the Horner product over the segments
+// The batch check's Miller loop, split by loop position (a lone lane carrying the six key pairs took
+// 39 ms, as long as the whole per-proof loop at 64k): segment h of the loop's 66 positions (bits
+// 63..0 -- a doubling step and an addition when set -- then the pi(Q), -pi^2(Q) additions) runs from
+// f = 1 (k_pghr_bseg). The loop's value is the Horner product over the segments
 //   (((seg[0])^(2^sq(1)) seg[1])^(2^sq(2)) ...) seg[S-1],  sq(h) = the doublings of segment h
 // which k_pghr_fe_coop forms after k_fe_easy's map x -> x^((p^6 - 1)(p^2 + 1)) (a homomorphism) has
 // put every seg[h] in the cyclotomic subgroup, where a squaring is Granger-Scott's.
 #define ZG_PGHR_FSEG 8
 #define ZG_FE_SLOTS 6  // the final exponentiation's per-value HBM workspace (k_fe_easy below)
 #define ZG_BN_POS (ZG_BN_ATE_BITS + 1)  // loop positions: q = 0 is bit 63, q = 64, 65 the two additions
-static_assert(ZG_PGHR_FSEG * ZG_BN_FIXED_Q <= 64, "one lane per (segment, pair)");
 ZG_INL int pghr_pos_bit(int q) { return ZG_BN_ATE_BITS - 2 - q; }
 ZG_INL int pghr_seg_lo(int h) { return h * ZG_BN_POS / ZG_PGHR_FSEG; }
 ZG_INL int pghr_seg_sq(int h) {  // doubling steps (squarings of f) in segment h
@@ -431,52 +525,36 @@ ZG_INL int pghr_seg_sq(int h) {  // doubling steps (squarings of f) in segment h
   for (int q = pghr_seg_lo(h); q < pghr_seg_lo(h + 1); q++) sq += pghr_pos_bit(q) >= 0;
   return sq;
 }
-__global__ void __launch_bounds__(64) k_pghr_fseg(const PghrPts* agg, const BLine* lines, Bq12* seg) {
-  __shared__ Bq12 sh[64];
-  const int t = threadIdx.x, h = t / ZG_BN_FIXED_Q, j = t % ZG_BN_FIXED_Q;
-  Bq12 f = b12_one();
-  if (h < ZG_PGHR_FSEG && !agg->p[j].inf) {
-    const BA1 p = agg->p[j];
-    const int q0 = pghr_seg_lo(h), q1 = pghr_seg_lo(h + 1);
-    int li = 0;
-    for (int q = 0; q < q0; q++) {
-      const int bit = pghr_pos_bit(q);
-      li += bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
-    }
-    for (int q = q0; q < q1; q++) {
-      const int bit = pghr_pos_bit(q);
-      if (bit >= 0 && q > q0) f = b12_sqr(f);  // the segment's first squaring is of 1 (counted in sq(h))
-      const int nsub = bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
-      for (int s = 0; s < nsub; s++, li++) f = b12_mul_bline(f, lines[(size_t)j * ZG_BN_NLINES + li], p);
-    }
-  }
-  sh[t] = f;
-  __syncthreads();
-  const bool seg_lane = h < ZG_PGHR_FSEG;
-  if (seg_lane && (j & 1) == 0) sh[t] = b12_mul(sh[t], sh[t + 1]);  // (01)(23)(45)
-  __syncthreads();
-  if (seg_lane && j == 0) seg[h] = b12_mul(b12_mul(sh[t], sh[t + 2]), sh[t + 4]);
-}
 #ifndef ZG_BSEG_WPE
 #define ZG_BSEG_WPE 1  // waves per SIMD the register budget allows (2 spills ~460 B/lane)
 #endif
-// grid (blocks of 64 lanes, ZG_PGHR_FSEG): lane g carries the proofs g, g + G, .., g + (K - 1) G
-// (G = ceil(n / K): a wave's line loads stay contiguous) over segment h = blockIdx.y as ONE
-// multi-pair loop -- a squaring shared by its K proofs per doubling step, then each proof's lines --
-// and the block multiplies its 64 values -> part[h gridDim.x + block] (1 where no proof is OK).
+// grid (1 + blocks of 64 lanes, S), segment h = blockIdx.y; each lane runs ONE multi-pair loop over
+// its segment -- a squaring per doubling step shared by all its pairs, then each pair's line:
+//  * block 0, lanes 0..5: key pair j on the batch's operand sums agg (lines from the key's table);
+//    the block is dispatched first, so it never waits behind the proofs' blocks (as a one-block
+//    kernel on a second stream, k_pghr_fseg, it waited for a free SIMD: 1.4 -> 5.2 ms);
+//  * block 1 + b, lane l: group g = 64 b + l carries the proofs g, g + G, .., g + (K - 1) G
+//    (G = ceil(n / K): a wave's line loads stay contiguous), lines from k_pghr_blines.
+// Each block multiplies its 64 values -> part[h gridDim.x + block] (1 where nothing takes part).
 // The Horner product over segments is multiplicative,
 //   prod_i Horner(s_i0, .., s_i7) = Horner(prod_i s_i0, .., prod_i s_i7),
-// so the b pairs join the key pairs segment by segment (k_pghr_segmul) and share their Horner
-// squarings and final exponentiation. (The key pairs as lanes of this grid instead, after their
-// operand sums on this stream: 64k 31.7 -> 33.1 ms, 8k 14.6 -> 16.3, profiles/r03y_pghr13_bench.txt.)
+// so one product tree per segment joins every pair of the batch before the shared Horner squarings
+// and final exponentiation.
 __global__ void __launch_bounds__(64, ZG_BSEG_WPE) k_pghr_bseg(int n, int K, const PghrPts* pts, const uint8_t* status,
-                                                               const BLine* bl, Bq12* part) {
+                                                               const BLine* bl, const PghrPts* agg,
+                                                               const BLine* klines, Bq12* part) {
   __shared__ Bq12 sh[64];
-  const int g = blockIdx.x * 64 + threadIdx.x, h = blockIdx.y, G = (n + K - 1) / K;
-  uint32_t live = 0;  // proof k of the lane takes part
-  for (int k = 0; k < K; k++) {
-    const int i = g + k * G;
-    if (g < G && i < n && status[i] == ZG_STATUS_OK && !pts[i].p[6].inf) live |= 1u << k;
+  const bool key = blockIdx.x == 0;  // block-uniform
+  const int g = ((int)blockIdx.x - 1) * 64 + threadIdx.x, h = blockIdx.y, G = (n + K - 1) / K;
+  const int np = key ? 1 : K;  // a key lane carries one pair (lane j < 6: pair j)
+  uint32_t live = 0;            // pair k of the lane takes part
+  for (int k = 0; k < np; k++) {
+    if (key) {
+      if (threadIdx.x < ZG_BN_FIXED_Q && !agg->p[threadIdx.x].inf) live = 1;
+    } else {
+      const int i = g + k * G;
+      if (g < G && i < n && status[i] == ZG_STATUS_OK && !pts[i].p[6].inf) live |= 1u << k;
+    }
   }
   Bq12 f = b12_one();
   if (live) {
@@ -488,13 +566,17 @@ __global__ void __launch_bounds__(64, ZG_BSEG_WPE) k_pghr_bseg(int n, int K, con
     }
     for (int q = q0; q < q1; q++) {
       const int bit = pghr_pos_bit(q);
-      if (bit >= 0 && q > q0) f = b12_sqr(f);  // as k_pghr_fseg
+      if (bit >= 0 && q > q0) f = b12_sqr(f);  // the segment's first squaring is of 1 (counted in sq(h))
       const int nsub = bit >= 0 && bn_ate_bit(bit) ? 2 : 1;
       for (int s = 0; s < nsub; s++, li++)
-        for (int k = 0; k < K; k++) {
+        for (int k = 0; k < np; k++) {
           if (!((live >> k) & 1u)) continue;
+          // one call site for both kinds of lane (two inlined copies of the sparse product cost
+          // the kernel its instruction cache)
           const size_t i = (size_t)g + (size_t)k * G;
-          f = b12_mul_bline(f, bl[(size_t)li * n + i], pts[i].p[6]);
+          const BLine* l = key ? klines + (size_t)threadIdx.x * ZG_BN_NLINES + li : bl + (size_t)li * n + i;
+          const BA1* p = key ? &agg->p[threadIdx.x] : &pts[i].p[6];
+          f = b12_mul_bline(f, *l, *p);
         }
     }
   }
@@ -506,11 +588,11 @@ __global__ void __launch_bounds__(64, ZG_BSEG_WPE) k_pghr_bseg(int n, int K, con
   }
   if (threadIdx.x == 0) part[(size_t)h * gridDim.x + blockIdx.x] = sh[0];
 }
-// seg[h] *= b[h stride] (the b pairs' segment products), seg[S] = 1 (k_fe_easy / k_pghr_fe_coop
-// keep their S + 1 inputs)
-__global__ void __launch_bounds__(64) k_pghr_segmul(Bq12* seg, const Bq12* b, size_t stride) {
+// the per-segment tree roots b[h stride] -> seg[h], seg[S] = 1 (k_fe_easy / k_pghr_fe_coop keep
+// their S + 1 inputs)
+__global__ void __launch_bounds__(64) k_pghr_segcopy(Bq12* seg, const Bq12* b, size_t stride) {
   const int h = threadIdx.x;
-  if (h < ZG_PGHR_FSEG) seg[h] = b12_mul(seg[h], b[stride * h]);
+  if (h < ZG_PGHR_FSEG) seg[h] = b[stride * h];
   if (h == ZG_PGHR_FSEG) seg[h] = b12_one();
 }
 // one level of the product tree over the block products: dst[k] = src[2k] * src[2k + 1] (an odd
@@ -708,7 +790,7 @@ __device__ void bc_exp_by_neg_u(BcWS* ws, int dst, int src, int tmp) {
   bc_copy(ws, dst, tmp, true);
 }
 // w: slot 0 of lanes 0..S of k_fe_easy's workspace (the segments' values and the b pairs' product,
-// each mapped into the cyclotomic subgroup) -> the Horner product (k_pghr_fseg's note), its hard part,
+// each mapped into the cyclotomic subgroup) -> the Horner product (k_pghr_bseg's note), its hard part,
 // status[0] = OK iff the result is 1
 __global__ void __launch_bounds__(64) k_pghr_fe_coop(const Bq12* w, uint8_t* status) {
   __shared__ BcWS ws;
@@ -982,7 +1064,7 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   PghrPts *dpts, *dagg;
   PghrDec* ddec;
   BA1* dmul;
-  BJ1 *daccp, *dpart;
+  BJ1 *daccp, *dpart, *dstr;
   BLine* dbl;
   Bq12 *df, *dw, *dbseg, *dbtmp, *dseg, *dbw;
   const Part parts[] = {
@@ -999,10 +1081,11 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
       {(void**)&df, sizeof(Bq12) * 2 * n},
       {(void**)&dw, sizeof(Bq12) * ZG_FE_SLOTS * n},
       {(void**)&dbl, sizeof(BLine) * ZG_BN_NLINES * n},
-      {(void**)&dpart, sizeof(BJ1) * ZG_BN_FIXED_Q * nb},
+      {(void**)&dpart, sizeof(BJ1) * ZG_BN_FIXED_Q * (nb + 4 * n / ZG_PGHR_SSUM_CH + 1)},
+      {(void**)&dstr, sizeof(BJ1) * ZG_PGHR_NFAM * n},
       {(void**)&dagg, sizeof(PghrPts)},
-      {(void**)&dbseg, sizeof(Bq12) * ZG_PGHR_FSEG * nb},
-      {(void**)&dbtmp, sizeof(Bq12) * ZG_PGHR_FSEG * nb},
+      {(void**)&dbseg, sizeof(Bq12) * ZG_PGHR_FSEG * (nb + 1)},
+      {(void**)&dbtmp, sizeof(Bq12) * ZG_PGHR_FSEG * (nb + 1)},
       {(void**)&dseg, sizeof(Bq12) * (ZG_PGHR_FSEG + 1)},
       {(void**)&dbw, sizeof(Bq12) * ZG_FE_SLOTS * (ZG_PGHR_FSEG + 1)},
       {(void**)&dbst, ZG_PGHR_FSEG + 1},
@@ -1023,14 +1106,14 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
     bump += (q.b + 255) & ~(size_t)255;
   }
   struct Events {
-    hipEvent_t e[6] = {};
+    hipEvent_t e[8] = {};
     ~Events() {
       for (hipEvent_t x : e)
         if (x) hipEventDestroy(x);
     }
   } ev;
-  hipEvent_t &e0 = ev.e[0], &e1 = ev.e[1], &fork = ev.e[2], &join = ev.e[3], &g2fork = ev.e[4], &g2join = ev.e[5];
-  for (hipEvent_t* x : {&fork, &join, &g2fork, &g2join}) BCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
+  hipEvent_t &e0 = ev.e[0], &e1 = ev.e[1], &g2fork = ev.e[4], &g2join = ev.e[5], &g2dec = ev.e[6], &stready = ev.e[7];
+  for (hipEvent_t* x : {&g2fork, &g2join, &g2dec, &stready}) BCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
   BCHK(hipMemcpyAsync(dp, proofs, 296 * n, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(din, inputs, 9 * 32 * n, hipMemcpyHostToDevice, st));
   BCHK(hipMemcpyAsync(drho, rho, ZG_PGHR_RHO_BYTES * n, hipMemcpyHostToDevice, st));
@@ -1045,38 +1128,52 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   BCHK(hipEventRecord(g2fork, st));
   BCHK(hipStreamWaitEvent(side, g2fork, 0));
   hipLaunchKernelGGL(k_pghr_decode_g2, dim3(nb), dim3(64), 0, side, (int)n, dp, ddec, dokb);
+  BCHK(hipGetLastError());
+  BCHK(hipEventRecord(g2dec, side));
   hipLaunchKernelGGL(k_pghr_blines, dim3(nb), dim3(64), 0, side, (int)n, ddec, dokb, dbl);
   BCHK(hipGetLastError());
-  BCHK(hipEventRecord(g2join, side));
-  hipLaunchKernelGGL(k_pghr_decode_g1, dim3(nb), dim3(448), 0, st, (int)n, dp, ddec, dokb);
+  // one-wave blocks: a multi-wave block must find all its waves' registers on one CU, and beside the
+  // side stream's ~280-register G2 waves it waited for them to finish (the 576-lane combs: 1.4 ->
+  // 10.5 ms, profiles/r03s3_pghr_timeline.txt)
+  hipLaunchKernelGGL(k_pghr_decode_g1, dim3(nb, 7), dim3(64), 0, st, (int)n, dp, ddec, dokb);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_accp, dim3(nb), dim3(576), 0, st, (int)n, din, dni, d->vk, d->comb, daccp);
+  hipLaunchKernelGGL(k_pghr_accp, dim3(nb, 9), dim3(64), 0, st, (int)n, din, dni, d->vk, d->comb, daccp);
   BCHK(hipGetLastError());
   hipLaunchKernelGGL(k_pghr_prep, dim3(nb), dim3(64), 0, st, (int)n, din, dni, d->vk, dokb, daccp, ddec, dst);
   BCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_pghr_rho, dim3(nb), dim3(64 * ZG_PGHR_NMUL), 0, st, (int)n, ddec, drho, dst, dmul);
-  BCHK(hipGetLastError());
-  BCHK(hipStreamWaitEvent(st, g2join, 0));
+  BCHK(hipStreamWaitEvent(st, g2dec, 0));  // the final statuses (b's decode verdict joins)
   hipLaunchKernelGGL(k_pghr_g2status, dim3(nb), dim3(64), 0, st, (int)n, dokb, dst);
-  hipLaunchKernelGGL(k_pghr_combine, dim3(nb), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
+  // side stream, after the b lines: the b pairs' operands P_i7 (one GLV product + combs per proof)
+  BCHK(hipEventRecord(stready, st));
+  BCHK(hipStreamWaitEvent(side, stready, 0));
+  hipLaunchKernelGGL(k_pghr_p7, dim3(nb), dim3(64), 0, side, (int)n, ddec, drho, d->comb, dst, dpts);
   BCHK(hipGetLastError());
-  // the batch check. Side stream: the six fixed pairs' operand sums and their loop by segments
-  // (single-wave kernels) -> dseg[0..S). Main stream, concurrently: the b pairs' segment values
-  // (from k_pghr_blines' lines) and one product tree per segment -> B_h; then dseg[h] *= B_h, the
-  // easy part of the S values, their Horner product and ONE hard part.
-  BCHK(hipEventRecord(fork, st));
-  BCHK(hipStreamWaitEvent(side, fork, 0));
-  BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, side));
-  hipLaunchKernelGGL(k_pghr_bsum, dim3(nb), dim3(64), 0, side, (int)n, dpts, dst, dpart);
-  hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, side, (int)nb, dpart, dagg);
-  hipLaunchKernelGGL(k_pghr_fseg, dim3(1), dim3(64), 0, side, dagg, d->lines, dseg);
+  BCHK(hipEventRecord(g2join, side));
+  // the six key pairs' operand sums (Straus over the GLV halves, B proofs per lane), concurrent with
+  // the side stream's b lines and P_i7
+  const int B = straus_b(n);
+  const long long G = ((long long)n + B - 1) / B;
+  const dim3 sg((unsigned)((G + 63) / 64), ZG_PGHR_NFAM);
+  if (B == 4)
+    hipLaunchKernelGGL(k_pghr_straus<4>, sg, dim3(64), 0, st, (int)n, ddec, drho, dst, dstr);
+  else if (B == 2)
+    hipLaunchKernelGGL(k_pghr_straus<2>, sg, dim3(64), 0, st, (int)n, ddec, drho, dst, dstr);
+  else
+    hipLaunchKernelGGL(k_pghr_straus<1>, sg, dim3(64), 0, st, (int)n, ddec, drho, dst, dstr);
   BCHK(hipGetLastError());
-  BCHK(hipEventRecord(join, side));
-  // proofs per bseg lane: enough lanes for ~8 waves per SIMD... of the 1-wave-per-SIMD kernel, the
-  // rest as shared squarings (K proofs per squaring)
+  const unsigned nch = (unsigned)((4 * G + ZG_PGHR_SSUM_CH - 1) / ZG_PGHR_SSUM_CH);
+  hipLaunchKernelGGL(k_pghr_ssum, dim3(ZG_BN_FIXED_Q, nch), dim3(64), 0, st, (int)G, dstr, dpart);
+  hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, st, (int)nch, dpart, dagg);
+  BCHK(hipGetLastError());
+  // the batch check: every pair of the batch by loop segment (k_pghr_bseg: the key pairs on the sums
+  // in block 0, the b pairs from the side stream's lines) and one product tree per segment ->
+  // dseg[0..S); the easy part of the S values, their Horner product and ONE hard part
+  BCHK(hipMemsetAsync(dbst, ZG_STATUS_OK, ZG_PGHR_FSEG + 1, st));
+  BCHK(hipStreamWaitEvent(st, g2join, 0));
   const int K = bseg_k(n);
-  const unsigned gb = bn_blocks(((long long)n + K - 1) / K);
-  hipLaunchKernelGGL(k_pghr_bseg, dim3(gb, ZG_PGHR_FSEG), dim3(64), 0, st, (int)n, K, dpts, dst, dbl, dbseg);
+  const unsigned gb = 1 + bn_blocks(((long long)n + K - 1) / K);  // + the key pairs' block
+  hipLaunchKernelGGL(k_pghr_bseg, dim3(gb, ZG_PGHR_FSEG), dim3(64), 0, st, (int)n, K, dpts, dst, dbl, dagg, d->lines,
+                     dbseg);
   BCHK(hipGetLastError());
   const size_t stride = gb;  // tree h over dbseg[h gb ..), dbtmp[h gb ..)
   Bq12 *src = dbseg, *dstb = dbtmp;
@@ -1085,8 +1182,7 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
     std::swap(src, dstb);
   }
   BCHK(hipGetLastError());
-  BCHK(hipStreamWaitEvent(st, join, 0));
-  hipLaunchKernelGGL(k_pghr_segmul, dim3(1), dim3(64), 0, st, dseg, src, stride);
+  hipLaunchKernelGGL(k_pghr_segcopy, dim3(1), dim3(64), 0, st, dseg, src, stride);
   hipLaunchKernelGGL(k_fe_easy, dim3(1), dim3(64), 0, st, ZG_PGHR_FSEG + 1, dseg, dbst, dbw, 1);
   hipLaunchKernelGGL(k_pghr_fe_coop, dim3(1), dim3(64), 0, st, dbw, dbst);
   BCHK(hipGetLastError());
@@ -1095,6 +1191,9 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   BCHK(hipStreamSynchronize(st));
   if (batch_failed) *batch_failed = bok != ZG_STATUS_OK;
   if (bok != ZG_STATUS_OK) {  // some proof fails: the per-proof path for the exact statuses
+    hipLaunchKernelGGL(k_pghr_rho, dim3(nb), dim3(64 * ZG_PGHR_NMUL), 0, st, (int)n, ddec, drho, dst, dmul);
+    hipLaunchKernelGGL(k_pghr_combine, dim3(nb), dim3(64), 0, st, (int)n, ddec, dmul, drho, d->comb, dst, dpts);
+    BCHK(hipGetLastError());
     const int halves = n < ZG_PGHR_SPLIT_BELOW ? 2 : 1;
     hipLaunchKernelGGL(k_pghr_miller, dim3(nb), dim3(64 * halves), 0, st, (int)n, dpts, d->lines, dst, df, halves);
     BCHK(hipGetLastError());
