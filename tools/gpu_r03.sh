@@ -71,6 +71,10 @@ for s in $STEPS; do
       ZG_STRAUS_B=$b timeout -k 10 200 python3 -u tools/bench_pghr13.py --no-cpu --n $n > $O/pghrb_${b}_$n.json 2> $O/pghrb_${b}_$n.err || { echo "pghr bench B=$b failed"; tail -30 $O/pghrb_${b}_$n.err; exit 1; }
       echo "B=$b $(cat $O/pghrb_${b}_$n.json)"
     done; done ;;
+  pghr8k)
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pghr8k -o run -- python3 $R/tools/bench_pghr13.py --no-cpu --n 8192 --reps 2 > /dev/null 2> $O/prof_pghr8k.err || { echo "rocprof pghr 8k failed"; tail -30 $O/prof_pghr8k.err; exit 1; }
+    cd $R && python3 tools/timeline.py $O/prof_pghr8k/run_results.db k_pghr_decode_g1 $O/pghr8k_timeline.txt > /dev/null && rm -f $O/prof_pghr8k/run_results.db ;;
   pghrtests)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_pghr13.py tests/test_collector.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_pghr.log 2>&1 || { echo "gpu pghr tests failed"; tail -60 $O/gpu_tests_pghr.log; exit 1; }
     tail -3 $O/gpu_tests_pghr.log ;;
