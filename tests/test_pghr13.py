@@ -100,9 +100,10 @@ def test_host_bn254_pairing_matches_oracle():
 
 
 def test_host_g2_membership_psi_equals_order_check():
-    """the product's G2 membership test psi(Q) == [6u^2] Q (zg_bn254.h ba2_in_subgroup: half the
-    doublings) decides exactly like AffineG2::new's [r] Q == O (ba2_in_subgroup_r, the oracle):
-    G2 points, random twist points, and points of the cofactor subgroup ([r] of a twist point)"""
+    """the product's G2 membership test [u + 1] Q + psi([u] Q) + psi^2([u] Q) == psi^3([2u] Q)
+    (zg_bn254.h ba2_in_subgroup: a 63-bit scalar) decides exactly like AffineG2::new's [r] Q == O
+    (ba2_in_subgroup_r, the oracle): G2 points, random twist points, points of the cofactor subgroup
+    ([r] of a twist point) and a point of each prime order dividing the cofactor"""
     import ctypes
     import random
     from oracle import bn254 as BN
@@ -122,6 +123,17 @@ def test_host_g2_membership_psi_equals_order_check():
             c = BN.ec_mul(F, (x, y), BN.R)   # order divides the cofactor 2p - r
             if c is not None:
                 pts.append((c, False))
+    # a point of each prime order l | h' = 2p - r (the twist's cofactor is squarefree: every Sylow
+    # subgroup is cyclic, so one point per l pins the product's 63-bit test, zg_bn254.h
+    # ba2_in_subgroup, to reject the whole l-part)
+    h = 2 * BN.P - BN.R
+    primes = [10069, 5864401, 1875725156269, h // (10069 * 5864401 * 1875725156269)]
+    assert h == primes[0] * primes[1] * primes[2] * primes[3] and len(set(primes)) == 4
+    q = next(p for p, want in pts if not want and BN.ec_mul(F, p, BN.R) is not None)
+    for l in primes:
+        c = BN.ec_mul(F, q, BN.R * (h // l))
+        assert c is not None and BN.ec_mul(F, c, l) is None
+        pts.append((c, False))
     for (x, y), want in pts:
         res = (ctypes.c_int * 2)()
         assert L.zgt_bn_g2_membership(b32(x[0]), b32(x[1]), b32(y[0]), b32(y[1]), res) == 1

@@ -513,12 +513,12 @@ ZG_INL BA2 ba2_frob(const BA2& q) {
 }
 ZG_INL BA2 ba2_frob2(const BA2& q) { return {b2_mul(q.x, b2_c(BQ_FROB2_2)), b2_mul(q.y, b2_c(BQ_FROB2_3))}; }
 
-// G2 membership decided as psi(Q) == [6u^2] Q (a 127-bit scalar: half the doublings of [r] Q).
-// psi (untwist-Frobenius-twist, ba2_frob) satisfies psi^2 - t psi + p = 0 on E'(Fq2) and acts on G2
-// as [p] = [p mod r] = [6u^2]. The endomorphism psi - [6u^2] has degree (6u^2)^2 - t 6u^2 + p =
-// p - 6u^2 = r (t = 6u^2 + 1), so its kernel is exactly G2: for Q on the twist,
-// psi(Q) = [6u^2] Q  <=>  [r] Q = O (AffineG2::new). tests/test_pghr13.py compares the two.
-ZG_INL bool ba2_in_subgroup(const BA2& q) {
+// G2 membership as psi(Q) == [6u^2] Q (a 127-bit scalar: half the doublings of [r] Q; round 3's
+// first form, kept for the host test). psi (untwist-Frobenius-twist, ba2_frob) satisfies
+// psi^2 - t psi + p = 0 on E'(Fq2) and acts on G2 as [p] = [p mod r] = [6u^2]. The endomorphism
+// psi - [6u^2] has degree (6u^2)^2 - t 6u^2 + p = p - 6u^2 = r (t = 6u^2 + 1), so its kernel is
+// exactly G2: for Q on the twist, psi(Q) = [6u^2] Q  <=>  [r] Q = O (AffineG2::new).
+ZG_INL bool ba2_in_subgroup_6u2(const BA2& q) {
   static constexpr uint32_t SIX_U2[4] = {0xe87cfd46u, 0xf83e9682u, 0xeeb859fbu, 0x6f4d8248u};  // 6u^2
   BJ2 acc = {q.x, q.y, b2_one()};
   for (int i = 125; i >= 0; i--) {  // bit 126 is the leading one
@@ -529,6 +529,54 @@ ZG_INL bool ba2_in_subgroup(const BA2& q) {
   const BA2 s = ba2_frob(q);
   const Bq2 z2 = b2_sqr(acc.Z);
   return b2_eq(acc.X, b2_mul(s.x, z2)) && b2_eq(acc.Y, b2_mul(s.y, b2_mul(z2, acc.Z)));
+}
+// Jacobian p + q (add-2007-bl with the special cases), psi and psi^2 on Jacobian points (conjugation
+// is a field automorphism, so psi(X : Y : Z) = (conj X g2 : conj Y g3 : conj Z))
+ZG_INL bool bj2_is_inf(const BJ2& p) { return b2_is_zero(p.Z); }
+ZG_INL BJ2 bj2_add(const BJ2& p, const BJ2& q) {
+  if (bj2_is_inf(p)) return q;
+  if (bj2_is_inf(q)) return p;
+  const Bq2 Z1Z1 = b2_sqr(p.Z), Z2Z2 = b2_sqr(q.Z);
+  const Bq2 U1 = b2_mul(p.X, Z2Z2), U2 = b2_mul(q.X, Z1Z1);
+  const Bq2 S1 = b2_mul(b2_mul(p.Y, q.Z), Z2Z2), S2 = b2_mul(b2_mul(q.Y, p.Z), Z1Z1);
+  const Bq2 H = b2_sub(U2, U1), rr = b2_dbl(b2_sub(S2, S1));
+  if (b2_is_zero(H)) return b2_is_zero(rr) ? bj2_dbl(p) : BJ2{b2_one(), b2_one(), b2_zero()};
+  const Bq2 I = b2_sqr(b2_dbl(H)), J = b2_mul(H, I), V = b2_mul(U1, I);
+  const Bq2 X3 = b2_sub(b2_sub(b2_sqr(rr), J), b2_dbl(V));
+  const Bq2 Y3 = b2_sub(b2_mul(rr, b2_sub(V, X3)), b2_dbl(b2_mul(S1, J)));
+  const Bq2 Z3 = b2_mul(b2_sub(b2_sub(b2_sqr(b2_add(p.Z, q.Z)), Z1Z1), Z2Z2), H);
+  return {X3, Y3, Z3};
+}
+ZG_INL BJ2 bj2_psi(const BJ2& p) {
+  return {b2_mul(b2_conj(p.X), b2_c(BQ_FROB1_2)), b2_mul(b2_conj(p.Y), b2_c(BQ_FROB1_3)), b2_conj(p.Z)};
+}
+ZG_INL BJ2 bj2_psi2(const BJ2& p) { return {b2_mul(p.X, b2_c(BQ_FROB2_2)), b2_mul(p.Y, b2_c(BQ_FROB2_3)), p.Z}; }
+ZG_INL bool bj2_eq(const BJ2& p, const BJ2& q) {
+  if (bj2_is_inf(p) || bj2_is_inf(q)) return bj2_is_inf(p) && bj2_is_inf(q);
+  const Bq2 Z1Z1 = b2_sqr(p.Z), Z2Z2 = b2_sqr(q.Z);
+  return b2_eq(b2_mul(p.X, Z2Z2), b2_mul(q.X, Z1Z1)) &&
+         b2_eq(b2_mul(b2_mul(p.Y, q.Z), Z2Z2), b2_mul(b2_mul(q.Y, p.Z), Z1Z1));
+}
+// G2 membership (round 3) as  [u + 1] Q + psi([u] Q) + psi^2([u] Q) == psi^3([2u] Q)  -- a 63-bit
+// scalar, half the doublings of the psi == [6u^2] form (El Housni-Guillevic-Piellard's test for BN
+// curves). Why it is exact here: #E'(Fq2) = r h' with h' = 2p - r = 10069 * 5864401 * 1875725156269 *
+// (a 178-bit prime), all distinct primes != r, so every Sylow subgroup of E'(Fq2) is cyclic of prime
+// order and the endomorphism E = [u + 1] + psi [u] + psi^2 [u] - psi^3 [2u] acts on each as a
+// scalar. E vanishes on G2 and on no point of order l for each l | h' (checked on a generator of each
+// component: tests/test_pghr13.py::test_host_g2_membership_*), so ker E = G2 exactly and the test
+// decides like AffineG2::new's [r] Q = O.
+ZG_INL bool ba2_in_subgroup(const BA2& q) {
+  BJ2 a = {q.x, q.y, b2_one()};
+  for (int i = 61; i >= 0; i--) {  // [u] Q, u = BN_U (bit 62 the leading one)
+    a = bj2_dbl(a);
+    if ((BN_U >> i) & 1ull) a = bj2_add_aff(a, q);
+  }
+  const BJ2 pa = bj2_psi(a);
+  BJ2 l = bj2_add_aff(a, q);          // [u + 1] Q
+  l = bj2_add(l, pa);                  // + psi([u] Q)
+  l = bj2_add(l, bj2_psi(pa));         // + psi^2([u] Q)
+  const BJ2 r = bj2_psi(bj2_psi2(bj2_dbl(a)));  // psi^3([2u] Q)
+  return bj2_eq(l, r);
 }
 
 #define ZG_BN_ATE_BITS 65  // 6u + 2

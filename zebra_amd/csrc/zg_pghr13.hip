@@ -419,11 +419,12 @@ __global__ void __launch_bounds__(64) k_pghr_p7(int n, const PghrDec* dec, const
   pts[i].p[6] = bj1_to_aff(t);
   pts[i].qb = d.qb;
 }
-// B by size: enough (family, group) lanes for ~2 waves per SIMD, the rest as shared doublings
+// B by size: enough (family, group) lanes for ~2 waves per SIMD, the rest as shared doublings (B = 4
+// keeps its 4 x 3 points in scratch)
 static int straus_b(size_t n) {
   static const int forced = getenv("ZG_STRAUS_B") ? atoi(getenv("ZG_STRAUS_B")) : 0;
   if (forced == 1 || forced == 2 || forced == 4) return forced;
-  return n >= 57344 ? 4 : n >= 28672 ? 2 : 1;
+  return n >= 28672 ? 2 : 1;  // 64k: B = 1 / 2 / 4 28.6 / 28.1 / 30.0 ms (profiles/r03s5_pghr13_bench.txt)
 }
 
 // the multi-Miller loop of one proof's 7 pairs, split over two waves of a 128-lane block (the same
@@ -1143,11 +1144,16 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   BCHK(hipGetLastError());
   BCHK(hipStreamWaitEvent(st, g2dec, 0));  // the final statuses (b's decode verdict joins)
   hipLaunchKernelGGL(k_pghr_g2status, dim3(nb), dim3(64), 0, st, (int)n, dokb, dst);
-  // side stream, after the b lines: the b pairs' operands P_i7 (one GLV product + combs per proof)
-  BCHK(hipEventRecord(stready, st));
-  BCHK(hipStreamWaitEvent(side, stready, 0));
-  hipLaunchKernelGGL(k_pghr_p7, dim3(nb), dim3(64), 0, side, (int)n, ddec, drho, d->comb, dst, dpts);
-  BCHK(hipGetLastError());
+  // the b pairs' operands P_i7 (one GLV product + combs per proof): on the side stream after the b
+  // lines from 32k proofs, where the main stream's Straus sums are the longer chain; below, the side
+  // stream's G2 chain (128 waves of decodes and lines at 8k) is, and P_i7 follows the sums on main
+  const bool p7_side = n >= 32768;
+  if (p7_side) {
+    BCHK(hipEventRecord(stready, st));
+    BCHK(hipStreamWaitEvent(side, stready, 0));
+    hipLaunchKernelGGL(k_pghr_p7, dim3(nb), dim3(64), 0, side, (int)n, ddec, drho, d->comb, dst, dpts);
+    BCHK(hipGetLastError());
+  }
   BCHK(hipEventRecord(g2join, side));
   // the six key pairs' operand sums (Straus over the GLV halves, B proofs per lane), concurrent with
   // the side stream's b lines and P_i7
@@ -1165,6 +1171,10 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   hipLaunchKernelGGL(k_pghr_ssum, dim3(ZG_BN_FIXED_Q, nch), dim3(64), 0, st, (int)G, dstr, dpart);
   hipLaunchKernelGGL(k_pghr_bsum_final, dim3(ZG_BN_FIXED_Q), dim3(64), 0, st, (int)nch, dpart, dagg);
   BCHK(hipGetLastError());
+  if (!p7_side) {
+    hipLaunchKernelGGL(k_pghr_p7, dim3(nb), dim3(64), 0, st, (int)n, ddec, drho, d->comb, dst, dpts);
+    BCHK(hipGetLastError());
+  }
   // the batch check: every pair of the batch by loop segment (k_pghr_bseg: the key pairs on the sums
   // in block 0, the b pairs from the side stream's lines) and one product tree per segment ->
   // dseg[0..S); the easy part of the S values, their Horner product and ONE hard part
