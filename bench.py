@@ -171,6 +171,15 @@ def h2d_copy_ms(proofs, kinds, inputs, dev, reps=5):
     return out
 
 
+# PGHR13 batch path, BN254 Fq products per proof: 7 G1 decompressions (Fq sqrt ~315);
+# b's decode (norm-method Fq2 sqrt ~700 + the 63-bit G2 membership ~1,870); 9 input combs x 32 mixed
+# additions (11) + acc; the Straus sums (9 families: 64 shared doublings / B=2 + ~48 mixed additions +
+# q + phi(q)); P_i7 (one GLV product + 4 byte combs); b's 102 lines (64 doublings x 28 + 38 additions x
+# 40 in Fq); the segment loops (64 Fq12 squarings shared by K=8 proofs + 102 sparse products x 43)
+PGHR13_FQ_PER_PROOF = {"g1_decode": 2205, "g2_decode": 2570, "input_combs": 3312, "straus_sums": 7443,
+                       "p7": 1470, "b_lines": 3312, "segment_loops": 4674}
+
+
 def other_configs(ctx, src_proofs, src_kinds, reps=5):
     """SURVEY.md 8(d) configs 2 and 4 through the host-buffer API zg_verify_batch (PCIe copies,
     OS-RNG scalars and the exact per-proof statuses included): not the headline metric."""
@@ -502,6 +511,17 @@ def main():
         if not args.no_cpu:
             pg["cpu_baseline"] = bench_pghr13.cpu_baseline(4.0, cpu_threads(args.cpu_threads))
             pg["gpu_over_cpu"] = pg["proofs_per_s"] / pg["cpu_baseline"]["proofs_per_s"]
+        # roofline ESTIMATE for the side line: BN254 Fq products per proof of the batch path counted from
+        # its operations (2 x 8^2 u32 MACs each, the word-form unit like the headline's
+        # 2 x 12^2), over the call's kernel time, against the same measured v_mad_u64_u32 peak
+        w = PGHR13_FQ_PER_PROOF
+        ach = sum(w.values()) * 128 * pg["proofs"] / (pg["kernel_ms"] * 1e-3) / 1e12
+        pg["roofline_est"] = {"bound": "valu-int (v_mad_u64_u32)", "achieved": ach, "peak": peak / 1e12,
+                              "unit": "T u32-MAC/s", "frac": ach / (peak / 1e12), "traffic": None,
+                              "work_per_proof_bn_fq_mul": w,
+                              "note": "estimate: per-proof operation counts of the batch path (one check per call; "
+                                      "the per-segment trees and the one final exponentiation per call are not "
+                                      "counted), not measured instruction counts"}
         out["pghr13_sprout_proofs"] = pg
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(proofs, kinds, inputs, args.cpu_seconds, cpu_threads(args.cpu_threads))
