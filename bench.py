@@ -515,7 +515,7 @@ def main():
         # its operations (2 x 8^2 u32 MACs each, the word-form unit like the headline's
         # 2 x 12^2), over the call's kernel time, against the same measured v_mad_u64_u32 peak
         w = PGHR13_FQ_PER_PROOF
-        ach = sum(w.values()) * 128 * pg["proofs"] / (pg["kernel_ms"] * 1e-3) / 1e12
+        ach = sum(w.values()) * 128 * pg["proofs"] / (max(pg["kernel_ms"], 1e-6) * 1e-3) / 1e12
         pg["roofline_est"] = {"bound": "valu-int (v_mad_u64_u32)", "achieved": ach, "peak": peak / 1e12,
                               "unit": "T u32-MAC/s", "frac": ach / (peak / 1e12), "traffic": None,
                               "work_per_proof_bn_fq_mul": w,
