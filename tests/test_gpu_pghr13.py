@@ -166,3 +166,34 @@ last one partial: odd product trees), also through the packed buffers, then the 
                                        b"".join(b"".join(r) + bytes(32 * (9 - len(r))) for r in ins),
                                        bytes(len(r) for r in ins))
             assert packed == got
+
+
+@pytest.mark.gpu
+def test_gpu_pghr13_batch_check_large(ctx):
+    """the large-call shapes of the batch path (40,000 proofs: Straus sums two proofs per lane, four
+    proofs per segment lane, P_i7 on the side stream -- zg_pghr13.hip straus_b / bseg_k / p7_side):
+    all valid (decided by the batch check alone), then with failing and decode-invalid cases mixed
+    in (the per-proof path's exact statuses)"""
+    from zebra_amd import zg
+    cases = GOLDEN["cases"]
+    valid = [c for c in cases if c["status"] == zg.STATUS_OK]
+    other = [c for c in cases if c["status"] != zg.STATUS_OK]
+    rnd = random.Random(41)
+    n = 40000
+    batch = [valid[rnd.randrange(len(valid))] for _ in range(n)]
+
+    def run(b):
+        ins = [_inputs(c) for c in b]
+        st0 = ctx.stats()
+        got = ctx.pghr13_verify(b"".join(bytes.fromhex(c["proof"]) for c in b),
+                                b"".join(b"".join(r) + bytes(32 * (9 - len(r))) for r in ins),
+                                bytes(len(r) for r in ins))
+        return got, ctx.stats()["pghr13_batch_failures"] - st0["pghr13_batch_failures"]
+
+    got, fails = run(batch)
+    assert got == [0] * n and fails == 0
+    for c in other:
+        batch[rnd.randrange(n)] = c
+    got, fails = run(batch)
+    assert got == [c["status"] for c in batch]
+    assert fails == (1 if any(c["status"] == zg.STATUS_VERIFY_FAILED for c in other) else 0)
