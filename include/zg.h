@@ -256,7 +256,10 @@ int zg_tree_roots_device(zg_ctx* ctx, int kind, int height, const uint8_t* state
  *        (-> ErrorKind::InvalidEncoding), ZG_STATUS_VERIFY_FAILED (-> InvalidPGHRProof),
  *        ZG_STATUS_INPUT_NONCANONICAL (an input >= r: not constructible as bn::Fr). The five
  *        pairing equalities of a proof are checked as one product with OS-random 128-bit weights
- *        (false accept ~2^-128). kernel_ms optional: device time of the three kernels.
+ *        (false accept ~2^-128). One batch check per chunk of at most 65,536 proofs (the
+ *        call's device scratch stays bounded however large n is). kernel_ms optional: device
+ *        time of the kernels, summed over the chunks. A key is freed from the device cache once
+ *        no context points at it (a context that loads another key, or is destroyed).
  *   zg_bn254_pairing (tests): e(P, Q) to the power 2u(6u^2 + 3u + 1) (the device's final
  *        exponentiation, see zg_bn254.h): P n x 64 (x, y), Q n x 128 (x.c0, x.c1, y.c0, y.c1),
  *        canonical little-endian Fq; GT n x 384 (12 Fq, coefficients of w^0..w^5 as c0, c1). */

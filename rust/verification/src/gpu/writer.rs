@@ -32,8 +32,9 @@ pub enum WriterError {
     /// the first failing block's error: its own checks, or (tx index, collector error)
     Verification(String),
     Database(String),
-    /// the window could not be verified (GPU error): nothing of the window was inserted; the
-    /// caller re-runs it on the CPU backend (collect::verify_block_or_cpu) or aborts the import
+    /// the window could not be verified (GPU error): nothing of the window was inserted and the
+    /// window is still held by the writer; the caller re-runs it on another backend
+    /// (`DeferredBlocksWriter::flush_with`, e.g. the CPU backend of cpu.rs) or aborts the import
     Backend(GpuError),
 }
 
@@ -155,26 +156,39 @@ impl<'a, S: BlockStore<B>, B: ImportBlock, V: Backend> DeferredBlocksWriter<'a, 
 
     /// verify the window, insert its blocks up to the first failing one, return its error
     pub fn flush(&mut self) -> Result<(), WriterError> {
+        let backend = self.backend;
+        self.flush_on(backend)
+    }
+
+    /// after `WriterError::Backend`: verify the window the writer still holds on another backend
+    /// (the CPU backend of cpu.rs), with the same insertion and first-error contract as `flush`
+    pub fn flush_with<W: Backend>(&mut self, other: &W) -> Result<(), WriterError> {
+        self.flush_on(other)
+    }
+
+    fn flush_on<W: Backend>(&mut self, backend: &W) -> Result<(), WriterError> {
         if self.window.is_empty() {
             return Ok(());
         }
-        let blocks = std::mem::take(&mut self.window);
-        self.pending.clear();
         // the window's transactions, flattened in block order (one verify_block call)
         let mut owner = Vec::new();
         let mut flat: Vec<&Tx> = Vec::new();
-        for (bi, b) in blocks.iter().enumerate() {
+        for (bi, b) in self.window.iter().enumerate() {
             for (ti, t) in b.txs().iter().enumerate() {
                 flat.push(t);
                 owner.push((bi, ti));
             }
         }
+        // verify BEFORE the window is taken: on a backend failure the window and the pending
+        // set stay as they were, so `retry_on` (or a later flush) can still verify them
         let res: Option<(usize, TxError)> = if flat.is_empty() {
             None
         } else {
             let txs: Vec<Tx> = flat.into_iter().map(clone_tx).collect();
-            verify_block(self.backend, &txs).map_err(WriterError::Backend)?
+            verify_block(backend, &txs).map_err(WriterError::Backend)?
         };
+        let blocks = std::mem::take(&mut self.window);
+        self.pending.clear();
         let (fail_block, err) = match res {
             None => (blocks.len(), None),
             Some((idx, e)) => {

@@ -176,3 +176,40 @@ def test_deferred_equals_sequential_with_forks(cpu_verify, seed):
     assert any(h.startswith("f") for h in want[0]) or want[1] is not None
     for window in (1, 5, 10 ** 6):
         assert run(DeferredBlocksWriter, stream, **deferred_kw(cpu_verify, window)) == want, (seed, window)
+
+
+def test_backend_failure_keeps_the_window(cpu_verify):
+    """a window whose verification raises (a GPU error) is neither dropped nor
+    inserted; the writer still holds it, so a retried flush (here: the backend recovers after
+    two failures) ends with exactly the sequential writer's storage and first error"""
+    from zebra_amd.blocks_writer import DeferredBlocksWriter, MemoryStorage, SequentialBlocksWriter
+    from zebra_amd.collector import verify_block
+    F = fields()
+    blocks = chain(12, 5, F, bad_proof={9}, orphan_swaps=2)
+    want = run(SequentialBlocksWriter, blocks, **seq_kw(cpu_verify))
+    fails = {"left": 2}
+
+    class GpuError(RuntimeError):
+        pass
+
+    def flaky(txs):
+        if fails["left"]:
+            fails["left"] -= 1
+            raise GpuError("device lost")
+        return verify_block(txs, verify=cpu_verify)
+    st = MemoryStorage("g")
+    w = DeferredBlocksWriter(st, verify_window=flaky, window_proofs=10 ** 6)
+    for b in blocks:
+        w.append_block(b)
+    held = list(w.window)
+    for _ in range(2):
+        with pytest.raises(GpuError):
+            w.flush()
+        assert w.window == held and st.blocks == ["g"]
+        assert all(w._known(b.hash) for b in held)
+    err = None
+    try:
+        w.flush()
+    except Exception as e:  # WriterError
+        err = e
+    assert (st.blocks, err) == want

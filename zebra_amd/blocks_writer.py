@@ -161,13 +161,16 @@ class DeferredBlocksWriter:
         """verify the window, insert its blocks up to the first failing one, raise its error"""
         if not self.window:
             return
-        blocks, self.window, self.pending = self.window, [], set()
+        blocks = self.window
         flat, owner = [], []
         for bi, b in enumerate(blocks):
             for ti, t in enumerate(b.txs):
                 flat.append(t)
                 owner.append((bi, ti))
+        # verify BEFORE the window is taken: a backend failure (GPU error) raises with the window
+        # and the pending set unchanged, so the caller can retry or re-run it on another backend
         res = self.verify_window(flat) if flat else None
+        self.window, self.pending = [], set()
         fail_block = len(blocks)
         err = None
         if res is not None:

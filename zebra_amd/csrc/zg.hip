@@ -53,6 +53,7 @@ struct BnKey;
 BnDev* bn_dev_new();
 void bn_dev_free(BnDev* d);
 int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, const BnKey** out, std::string* err);
+void bn_key_release(BnDev* d, const BnKey* k);
 int bn_pghr13_verify(const BnKey* k, hipStream_t st, hipStream_t side, size_t n, const uint8_t* proofs,
                      const uint8_t* inputs, const uint8_t* ninputs, const uint8_t* rho, uint8_t* status,
                      float* kernel_ms, bool* batch_failed, void** arena, size_t* arena_cap, std::string* err);
@@ -160,7 +161,7 @@ struct zg_ctx {
   uint64_t calls = 0;
   int debug_each = 0;         // ZG_DEBUG_EACH=1: every batch's statuses re-checked per proof
   uint8_t* d_dbg = nullptr;   // the per-proof statuses of that re-check
-  const zg::BnKey* bn_key = nullptr;  // this slot's PGHR13 key (an immutable entry of the device cache)
+  const zg::BnKey* bn_key = nullptr;  // this slot's PGHR13 key (an immutable, reference-counted entry of the device cache)
   void* tree_arena = nullptr;  // zg_tree_roots scratch (grow-only, zg_merkle.hip)
   size_t tree_arena_cap = 0;
   void* bn_arena = nullptr;  // zg_pghr13_verify scratch (grow-only, zg_pghr13.hip)
@@ -331,6 +332,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   // the pool's streams outlive the slot: drain this slot's work before its buffers go
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
+  if (ctx->bn_key && ctx->dev) zg::bn_key_release(ctx->dev->bn, ctx->bn_key);
   void* ptrs[] = {ctx->d_vk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
@@ -1540,8 +1542,12 @@ static zg::BnDev* bn_dev(zg_ctx* ctx) {
 static int pghr13_load_locked(zg_ctx* ctx, const char* json, size_t len) {
   HIPCHK(hipSetDevice(ctx->device));
   const zg::BnKey* k = nullptr;
-  const int rc = bn_load_vk_json(bn_dev(ctx), ctx->stream, json, len, &k, &ctx->err);
-  if (rc == ZG_OK) ctx->bn_key = k;
+  zg::BnDev* d = bn_dev(ctx);
+  const int rc = bn_load_vk_json(d, ctx->stream, json, len, &k, &ctx->err);
+  if (rc == ZG_OK) {
+    if (ctx->bn_key) bn_key_release(d, ctx->bn_key);  // the old key goes once no context uses it
+    ctx->bn_key = k;
+  }
   return rc;
 }
 
@@ -1555,6 +1561,7 @@ extern "C" int zg_pghr13_vk_load_builtin(zg_ctx* ctx) {
   return zg_pghr13_vk_load_json(ctx, ZG_PGHR13_VK_JSON, strlen(ZG_PGHR13_VK_JSON));
 }
 
+#define ZG_PGHR_CHUNK ((size_t)65536)
 extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* inputs,
                                 const uint8_t* n_inputs, uint8_t* status, float* kernel_ms) {
   if (!ctx || (n && (!proofs || !inputs || !status)) || n > (1u << 24)) return ZG_E_INVAL;
@@ -1593,14 +1600,23 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
   } else if (!os_random(rho.data(), rho.size())) {
     return fail(ctx, ZG_E_INVAL, "getrandom failed");
   }
-  bool batch_failed = false;
-  const int rc = bn_pghr13_verify(ctx->bn_key, ctx->stream, ctx->side, n, proofs, inputs, n_inputs, rho.data(),
-                                  status, kernel_ms, &batch_failed, &ctx->bn_arena, &ctx->bn_arena_cap, &ctx->err);
-  if (rc == ZG_OK && n) {
+  // one batch check per chunk of at most ZG_PGHR_CHUNK proofs: the call's arena (~27 KB per proof,
+  // mostly the b lines) stays bounded at the chunk size however large the caller's window is
+  if (kernel_ms) *kernel_ms = 0;
+  for (size_t o = 0; o < n; o += ZG_PGHR_CHUNK) {
+    const size_t m = n - o < ZG_PGHR_CHUNK ? n - o : ZG_PGHR_CHUNK;
+    bool batch_failed = false;
+    float ms = 0;
+    const int rc = bn_pghr13_verify(ctx->bn_key, ctx->stream, ctx->side, m, proofs + 296 * o, inputs + 9 * 32 * o,
+                                    n_inputs ? n_inputs + o : nullptr, rho.data() + 80 * o, status + o,
+                                    kernel_ms ? &ms : nullptr, &batch_failed, &ctx->bn_arena, &ctx->bn_arena_cap,
+                                    &ctx->err);
+    if (rc != ZG_OK) return rc;
+    if (kernel_ms) *kernel_ms += ms;
     ctx->stats[8]++;
     if (batch_failed) ctx->stats[9]++;
   }
-  return rc;
+  return ZG_OK;
 }
 
 extern "C" int zg_bn254_pairing(zg_ctx* ctx, size_t n, const uint8_t* g1, const uint8_t* g2, uint8_t* gt) {

@@ -235,14 +235,20 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_Q4 : ZG_PROG_Q4SQ);
+      ZG_TRACE_S(n, 0);
       prog_run<true>(pid, at);
+      ZG_TRACE_S(n, 1);
       Fq2 v;
       if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      ZG_TRACE_S(n, 2);
       __syncthreads();
+      ZG_TRACE_S(n, 3);
       n++;
       if (wave < 6) at.put(wave, v);
       if (n < ZG_NCOEFF) load_lines(n);
+      ZG_TRACE_S(n - 1, 4);
       __syncthreads();
+      ZG_TRACE_S(n - 1, 5);
     }
     if (last) break;
   }

@@ -875,6 +875,7 @@ __global__ void __launch_bounds__(64) k_bn_gt(int n, Bq12* w, uint32_t* gt) {
 // context does not change the key of any other context).
 struct BnKey {
   std::vector<uint32_t> raw;  // the parsed key words (the cache key)
+  int refs = 0;               // contexts pointing at this entry (BnDev::mu); freed at 0
   BnVK* vk = nullptr;
   BLine* lines = nullptr;
   uint32_t* comb = nullptr;
@@ -894,6 +895,20 @@ static void bn_key_free(BnKey* k) {
 }
 
 BnDev* bn_dev_new() { return new BnDev(); }
+// a context stops pointing at k (it loaded another key, or it is destroyed): the entry and its HBM
+// (VK, line table, comb tables) go once no context uses it, so rotating keys does not grow the cache
+void bn_key_release(BnDev* d, const BnKey* k) {
+  if (!d || !k) return;
+  std::lock_guard<std::mutex> g(d->mu);
+  for (size_t i = 0; i < d->keys.size(); i++)
+    if (d->keys[i] == k) {
+      if (--d->keys[i]->refs == 0) {
+        bn_key_free(d->keys[i]);
+        d->keys.erase(d->keys.begin() + i);
+      }
+      return;
+    }
+}
 void bn_dev_free(BnDev* d) {
   if (!d) return;
   for (BnKey* k : d->keys) bn_key_free(k);
@@ -1006,6 +1021,7 @@ int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, cons
   std::lock_guard<std::mutex> g(d->mu);  // one build per distinct key, never a half-built entry visible
   for (BnKey* k : d->keys)
     if (k->raw == raw) {
+      k->refs++;
       *out = k;
       return ZG_OK;
     }
@@ -1044,6 +1060,7 @@ int bn_load_vk_json(BnDev* d, hipStream_t st, const char* json, size_t len, cons
     *err = "PGHR13 key: a point is not on its curve or not of order r (AffineG*::new)";
     return ZG_E_VK;
   }
+  k->refs = 1;
   d->keys.push_back(k);
   *out = k;
   return ZG_OK;
@@ -1126,6 +1143,12 @@ int bn_pghr13_verify(const BnKey* d, hipStream_t st, hipStream_t side, size_t n,
   }
   // b's decode (Fq2 sqrt + G2 membership) and its lines (lane per proof at ~280 registers: one
   // wave per SIMD) on the side stream, sharing the SIMDs with the G1 decodes, combs, prep and rho
+  // from the fork on, every return (an error included) first drains the side stream: its kernels
+  // use this call's arena, which the next call on this context reuses
+  struct SideJoin {
+    hipStream_t s;
+    ~SideJoin() { hipStreamSynchronize(s); }
+  } side_join{side};
   BCHK(hipEventRecord(g2fork, st));
   BCHK(hipStreamWaitEvent(side, g2fork, 0));
   hipLaunchKernelGGL(k_pghr_decode_g2, dim3(nb), dim3(64), 0, side, (int)n, dp, ddec, dokb);
