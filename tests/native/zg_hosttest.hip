@@ -69,7 +69,7 @@ void zgt_lines_lane(const uint8_t* q, const uint8_t* p, uint8_t* out_lane, uint8
     st_fq(v.c0, o);
     st_fq(v.c1, o + 48);
   };
-  G2J r = {B.x, B.y, f2_one()};
+  LinesHost r = {{B.x, B.y, f2_one()}};
   Fq2 l[3];
   int n = 0;
   for (int i = ZG_XH_TOP; i >= -1; i--) {

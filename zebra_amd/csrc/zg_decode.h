@@ -45,10 +45,14 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) 
   b.ptAC[(size_t)role * b.npad + i] = p;
 }
 
+// JOB < 0: every job in one launch (grid 4G); JOB = 0 / 1 / 2: that job alone (grid G / 2G / G,
+// ZG_DECODE_SPLIT=1: separate launches, so each job gets its own register budget and its own
+// kernel-trace line)
+template <int JOB>
 __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b) {
   const int G = (b.npad + 63) / 64;
-  const int blk = blockIdx.x;
-  const int job = blk < G ? 0 : blk < 3 * G ? 1 : 2;  // 0 GLV A, 1 subgroup, 2 B (wave-uniform)
+  const int blk = JOB < 0 ? (int)blockIdx.x : JOB == 0 ? (int)blockIdx.x : JOB == 1 ? G + (int)blockIdx.x : 3 * G + (int)blockIdx.x;
+  const int job = JOB >= 0 ? JOB : blk < G ? 0 : blk < 3 * G ? 1 : 2;  // 0 GLV A, 1 subgroup, 2 B (wave-uniform)
   const int role = job == 0 ? 0 : job == 2 ? 2 : ((blk - G) & 1);  // 0 A, 1 C, 2 B
   const int grp = job == 0 ? blk : job == 2 ? blk - 3 * G : (blk - G) >> 1;
   const int i = grp * 64 + (threadIdx.x & 63);

@@ -3,6 +3,7 @@
 // waves-per-SIMD register budget (a callee shared with other kernels is compiled for the
 // loosest budget of its callers).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "../../include/zg.h"
 #define ZG_DECODE_WPE 2
@@ -13,7 +14,14 @@ namespace zg {
 // G1 square roots, then the point jobs (GLV r_i A_i, subgroup checks, B), then per-proof statuses and Fr leaves
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b) {
   hipLaunchKernelGGL(k_decode_sqrt, dim3(2 * groups), dim3(64), 0, st, b);
-  hipLaunchKernelGGL(k_decode_points, dim3(4 * groups), dim3(64), 0, st, b);
+  static const int split = getenv("ZG_DECODE_SPLIT") ? atoi(getenv("ZG_DECODE_SPLIT")) : 0;
+  if (split) {
+    hipLaunchKernelGGL(k_decode_points<0>, dim3(groups), dim3(64), 0, st, b);
+    hipLaunchKernelGGL(k_decode_points<1>, dim3(2 * groups), dim3(64), 0, st, b);
+    hipLaunchKernelGGL(k_decode_points<2>, dim3(groups), dim3(64), 0, st, b);
+  } else {
+    hipLaunchKernelGGL(k_decode_points<-1>, dim3(4 * groups), dim3(64), 0, st, b);
+  }
   hipLaunchKernelGGL(k_decode_finish, dim3(groups), dim3(64), 0, st, b);
   return hipGetLastError();
 }

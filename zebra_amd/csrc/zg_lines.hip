@@ -26,17 +26,22 @@ __global__ void __launch_bounds__(64, WPE) k_batch_lines_lane(BatchBufs b, Fq2* 
   // point and one step's temporaries
   const G2A* pq = &b.ptB[chk ? proof : 0];
   const G1A* pa = &b.ptA[act ? proof : 0];
-  G2J r;
+  __shared__ uint4 lds_pt[3 * ZG_ATOM_ROWS * 64];  // X, Y, Z of the block's 64 proofs (18 KB)
+  AtomSpace st{lds_pt};
   if (chk) {
-    r = {pq->x, pq->y, f2_one()};
+    st.put(0, pq->x);
+    st.put(1, pq->y);
   } else {
-    r = {f2_one(), f2_one(), f2_one()};
+    st.put(0, f2_one());
+    st.put(1, f2_one());
   }
+  st.put(2, f2_one());
   int n = 0;
   for (int i = ZG_XH_TOP; i >= -1; i--) {
-    ls_double(r, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act);
-    if (i >= 0 && ((ZG_XH >> i) & 1ull)) ls_add(r, pq, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act && chk);
+    ls_double(st, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act);
+    if (i >= 0 && ((ZG_XH >> i) & 1ull)) ls_add(st, pq, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act && chk);
   }
+  const G2J r = {st.get(0), st.get(1), st.get(2)};
   // r = [x] B (Jacobian). B in G2  <=>  psi(B) = [u] B = -[x] B  <=>  X = psi_x Z^2, Y = -psi_y Z^3,
   // Z != 0 (the step formulas are exact unless they degenerate, which only a B outside G2 can
   // make happen, and then Z = 0)
