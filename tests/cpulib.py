@@ -39,6 +39,19 @@ def verify(L, proofs, kinds, inputs, n_inputs=None, threads=1, want_gt=False):
     return sts, ([gts.raw[576 * i:576 * i + 576] for i in range(n)] if want_gt else None)
 
 
+OPS = ("fq_mul_ns", "fq_sqr_ns", "miller_loop_3pair_us", "final_exp_us", "g2_prepare_us", "g1_mul255_us",
+       "g2_subgroup_us", "verify_one_us")
+
+
+def bench_ops(L, kind, proof, inputs, k, reps=20):
+    """single-thread timings of the port's building blocks (zgcpu_bench_ops), a dict over OPS"""
+    L.zgcpu_bench_ops.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]
+    out = (ctypes.c_double * 8)()
+    assert L.zgcpu_bench_ops(kind, bytes(proof), bytes(inputs), k, reps, out) == 0
+    return dict(zip(OPS, list(out)))
+
+
 def load_merkle():
     """oracle/_build/libzgmerkle.so (merkle_cpu.cpp), initialised with the Pedersen generators of
     the Python oracle"""

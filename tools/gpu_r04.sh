@@ -39,6 +39,15 @@ for s in $STEPS; do
   lanetest)
     timeout -k 10 400 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/lanetest.log 2>&1 || { echo "lane tests failed"; tail -40 $O/lanetest.log; exit 1; }
     tail -3 $O/lanetest.log ;;
+  wave8k)
+    # 8k shards (the 8-GPU per-rank size), 6 batches in flight: kernel trace -> wave-time shares
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace -d $O/prof8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 36 --warmup 6 > $O/prof8k.json 2> $O/prof8k.err || { echo "rocprof 8k failed"; tail -30 $O/prof8k.err; exit 1; }
+    cd $R && python3 tools/wavetime.py $O/prof8k/run_results.db $O/wavetime_8k.txt > /dev/null && rm -f $O/prof8k/run_results.db && head -30 $O/wavetime_8k.txt ;;
+  configs)
+    # the driver's default bench line incl. config 2 / config 4 side lines (no CPU leg)
+    timeout -k 10 400 python3 -u bench.py --no-cpu > $O/bench_configs.json 2> $O/bench_configs.err || { echo "bench configs failed"; tail -30 $O/bench_configs.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_configs.json')); print({k: d[k] for k in d if 'config' in k.lower() or k in ('value','ms_per_step')})" ;;
   quick)
     timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_quick.json 2> $O/bench_quick.err || { echo "bench quick failed"; tail -30 $O/bench_quick.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_quick.json')); print('64k', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"

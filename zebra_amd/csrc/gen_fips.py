@@ -182,7 +182,9 @@ def fq_ops_fn(name, kinds):
     lines = ["// %s: %s (%d instructions, %d s_nop)" % (name, ", ".join(kinds), len(text) - nops, nops),
              "__device__ __forceinline__ void %s(%s) {" % (name, args),
              "  uint32_t tmp[%d];" % max(1, len(temps)), "  uint64_t car[%d];" % len(carries),
-             '  asm volatile("%s"' % "\\n\\t".join(text),
+             # not volatile: a pure function of its operands (carries in explicit SGPR outputs, no
+             # implicit vcc), so the compiler may issue the LDS loads of a lazy form ahead of it
+             '  asm("%s"' % "\\n\\t".join(text),
              "               : " + ", ".join(outs),
              "               : " + ", ".join(ins) + ");", "}"]
     return lines

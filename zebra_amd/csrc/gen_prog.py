@@ -636,8 +636,34 @@ def red_of(M):
     return r if r <= 2 else 0
 
 
+HOIST = int(os.environ.get("ZG_GEN_HOIST", "0"))  # issue the first HOIST LDS / HBM atom loads of a product's operands before its first carry chain
+
+
+def hoist_loads(lines):
+    """move the atom loads (`const Fq2 v = at.get(s);` / `at.q(j)`) to the front, in order: the carry
+    chains are asm volatile, which the compiler does not move loads across, so a load emitted right
+    before its first use exposes one LDS round trip per atom; hoisted, they are all in flight at once"""
+    if not HOIST:
+        return lines
+    ld = [ln for ln in lines if ln.startswith("const Fq2 ") and (" = at.get(" in ln or " = at.q(" in ln)]
+    ld = ld[:HOIST]  # the first HOIST atoms (24 VGPRs each, live next to the forms' accumulators)
+    return ld + [ln for ln in lines if ln not in ld]
+
+
+HOIST_GLOBAL = int(os.environ.get("ZG_GEN_HOIST_GLOBAL", "1"))  # hoist over both operands (else per operand)
+
+
+def hoist_op(lines):
+    return lines if HOIST_GLOBAL else hoist_loads(lines)
+
+
 def lazy_product(L, R, kind, slot):
     """(lines, encoded kind expression) for one product"""
+    lines, code = _lazy_product(L, R, kind, slot)
+    return (hoist_loads(lines) if HOIST_GLOBAL else lines), code
+
+
+def _lazy_product(L, R, kind, slot):
     if kind == K_SQR:
         lx, bx = lazy_form(L, slot, "x", False)
         M = 4 * bx * bx
@@ -645,13 +671,13 @@ def lazy_product(L, R, kind, slot):
             lx.append("x = f2_reduce_q(x);")
             bx, M = 1, 4
         assert fits(M) and 2 * bx * P < 2 ** 384
-        return lx, "ZG_KIND(1, %d, %d)" % (bx, red_of(M))
+        return hoist_op(lx), "ZG_KIND(1, %d, %d)" % (bx, red_of(M))
     if kind in (K_MULC0, K_MULC1):
         assert len(R) == 1 and list(R.values())[0] == (1, 0), "the Fq factor is an input atom"
         lx, bx = lazy_form(L, slot, "x", False)
         ly, _ = lazy_form(R, slot, "y", False)
         assert fits(bx)
-        return lx + ly, "ZG_KIND(%d, 0, %d)" % (kind, red_of(bx))
+        return hoist_op(lx) + hoist_op(ly), "ZG_KIND(%d, 0, %d)" % (kind, red_of(bx))
     best = None
     for A, Bf in ((L, R), (R, L)):
         lx, bx = lazy_form(A, slot, "x", False)
@@ -672,7 +698,7 @@ def lazy_product(L, R, kind, slot):
             by = 1
         M = bx * (2 * by + 1)
     assert by + 1 <= KMAX and fits(M) and bx <= 9 and by <= 9
-    return lx + ly, "ZG_KIND(0, %d, %d)" % (by + 1, red_of(M))
+    return hoist_op(lx) + hoist_op(ly), "ZG_KIND(0, %d, %d)" % (by + 1, red_of(M))
 
 
 def _run_lines(lines, atoms, env):
@@ -824,6 +850,7 @@ def emit(specs):
                 out_cases.append("  case %d: return f2_zero();  // %s out %d: stored by its product" % (go + j, name, j))
             elif LAZY:
                 lines, _ = lazy_form(f, sch["slot"], "v", True)
+                lines = hoist_loads(lines)
                 out_cases.append("  case %d: {  // %s out %d\n    Fq2 v;\n    %s\n    return v;\n  }" % (
                     go + j, name, j, "\n    ".join(lines)))
             else:

@@ -6,7 +6,9 @@
 #include <stdlib.h>
 
 #include "../../include/zg.h"
+#ifndef ZG_DECODE_WPE
 #define ZG_DECODE_WPE 2
+#endif
 #include "zg_decode.h"
 
 namespace zg {
