@@ -295,7 +295,9 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
  * (k_batch_fchain4; shards of 8,192 or more padded proofs -- ZG_QUAD_MIN -- or as ZG_FCHAIN_QUADS
  * forces), [8] zg_pghr13_verify calls with proofs, [9] those whose one batch check failed (the
- * call then ran the per-proof check for the exact statuses). Writes min(n, 10) values, zero beyond. */
+ * call then ran the per-proof check for the exact statuses), [10] batches whose sums r_i C_i came
+ * from the GLV products in decode and the C-sum tree (shards below 16,384 padded proofs -- ZG_K4_MIN
+ * -- instead of K4's Pippenger buckets; [6] is 0 for them). Writes min(n, 11) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

@@ -28,9 +28,12 @@ using namespace zg;
 #define ZG_NODE_CHUNK 4096
 #define ZG_NEV 13
 #define ZG_NTIMINGS 9
-#define ZG_NSTATS 10
+#define ZG_NSTATS 11
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
+#define ZG_K4_MIN 16384          // shards from this many (padded) proofs sum r_i C_i by K4's Pippenger buckets;
+                                 // below, the GLV products in decode + the C tree levels (8k: K4's bucket grid
+                                 // held 17% of a batch's wave-time for ~1 ms of lone-lane addition chains)
 #define ZG_LINES_LANE_MIN 32768  // straight-line R-chain from here (r03: 64k 14.93 -> 14.47 ms per batch in
                                  // flight; 16k 4.90 -> 5.14 and 8k 3.21 -> 3.63 favour the staged program)
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
@@ -150,6 +153,8 @@ struct zg_ctx {
                             // 2; the staged program below), 1 / 2 always straight-line sized for 2 / 1
                             // waves per SIMD, 0 always the staged program (zg_kernels.h)
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
+  long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
+  int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
   hipEvent_t ev[ZG_NEV] = {};
@@ -270,6 +275,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
+  if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
   if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
   if (const char* e = getenv("ZG_DEBUG_EACH")) ctx->debug_each = atoi(e);
@@ -673,9 +679,9 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 }
 
 namespace zg {
-hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b);          // zg_decode.hip
+hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv);  // zg_decode.hip
 hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate,
-                           hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr);          // zg_msm.hip
+                           hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr, int k4 = 1);          // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
 hipError_t launch_lines_lane(unsigned groups, hipStream_t st, const BatchBufs& b, Fq2* lines, int wpe);  // zg_lines.hip
 // the staged-program kernels of zg_kernels.h, one translation unit each (zg_prog_*.hip)
@@ -703,6 +709,13 @@ hipError_t launch_sapling_bvk(hipStream_t st, int ntx, const uint32_t* off, cons
 // and f-chain kernels instead of extending the critical path. A B_i that fails its G2
 // subgroup check in k_batch_lines (invalid proofs only) counts in bfail, and the side-stream
 // results are then recomputed on the main stream (gated kernels: no-ops when bfail == 0).
+// the C-sum tree levels above the leaves (small shards: the GLV leaves k_decode_points wrote), root
+// ctree[1]; gate as for the recompute kernels (null: always)
+static hipError_t launch_c_tree(zg_ctx* ctx, const BatchBufs& b, hipStream_t st, const int* gate) {
+  for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2)
+    hipLaunchKernelGGL(k_tree_c, dim3(nblocks(lo * ZG_NKINDS)), dim3(ZG_BLOCK), 0, st, b, (int)lo, gate);
+  return hipGetLastError();
+}
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   static const int root = 1;
@@ -710,7 +723,9 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipMemsetAsync(b.bfail, 0, 2 * sizeof(int), ctx->stream));  // bfail, fused-wait failure
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
-  HIPCHK(launch_batch_decode(dgroups, ctx->stream, b));
+  const int k4 = (long)ctx->npad >= ctx->k4_min ? 1 : 0;
+  ctx->k4_last = k4;
+  HIPCHK(launch_batch_decode(dgroups, ctx->stream, b, !k4));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->trees_built = 0;
   ctx->c_tree_pending = 0;
@@ -718,7 +733,8 @@ static int run_pipeline(zg_ctx* ctx) {
   // side stream: K4 + the root's VK-side work (or, serial_side, on the main stream after the tree)
   auto side_work = [&](hipStream_t st) -> int {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
-    HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9]));
+    HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9], k4));
+    if (!k4) HIPCHK(launch_c_tree(ctx, b, st, nullptr));
     HIPCHK(hipEventRecord(ctx->ev[10], st));
     int r = launch_node_msm_pairs(ctx, b, nb, st);
     if (r) return r;
@@ -785,7 +801,8 @@ static int run_pipeline(zg_ctx* ctx) {
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream K4 + root pairs complete
   }
   // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
-  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail));
+  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail, nullptr, nullptr, k4));
+  if (!k4) HIPCHK(launch_c_tree(ctx, b, ctx->stream, b.bfail));
   rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
   if (rc) return rc;
   ctx->root_pairs_ready = 1;
@@ -949,7 +966,8 @@ static int collect_batch_stats(zg_ctx* ctx) {
     ctx->fuse_off = 1;
   }
   if (flags[0]) ctx->stats[3]++;
-  ctx->stats[6] = (uint64_t)entries;
+  ctx->stats[6] = ctx->k4_last ? (uint64_t)entries : 0;
+  if (!ctx->k4_last) ctx->stats[10]++;
   hipEventElapsedTime(&ctx->timings[0], ctx->ev[0], ctx->ev[1]);  // decode
   hipEventElapsedTime(&ctx->timings[1], ctx->ev[1], ctx->ev[7]);  // lines (R-chain)
   hipEventElapsedTime(&ctx->timings[2], ctx->ev[7], ctx->ev[2]);  // f-chain
@@ -1028,10 +1046,14 @@ static int build_trees(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
-  HIPCHK(launch_c_leaves(ctx->side, b));
+  // small shards (k4_last = 0): the pipeline already built the whole C tree from the GLV leaves
+  if (ctx->k4_last) HIPCHK(launch_c_leaves(ctx->side, b));
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2) {
-    hipLaunchKernelGGL(k_tree_c, dim3(nblocks(lo * ZG_NKINDS)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo);
-    HIPCHK(hipGetLastError());
+    if (ctx->k4_last) {
+      hipLaunchKernelGGL(k_tree_c, dim3(nblocks(lo * ZG_NKINDS)), dim3(ZG_BLOCK), 0, ctx->side, b, (int)lo,
+                         (const int*)nullptr);
+      HIPCHK(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_tree_s, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     HIPCHK(hipGetLastError());
   }

@@ -48,13 +48,19 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) 
 // JOB < 0: every job in one launch (grid 4G); JOB = 0 / 1 / 2: that job alone (grid G / 2G / G,
 // ZG_DECODE_SPLIT=1: separate launches, so each job gets its own register budget and its own
 // kernel-trace line)
+// cglv (small shards, ZG_K4_MIN): the GLV products r_i C_i run here too, as blocks [G, 2G) beside
+// those of A, and go to the C-sum tree leaves (ctree[npad + i], the proof's key; the other keys'
+// entries the point at infinity) -- the side stream then sums them by the tree levels instead of
+// K4's Pippenger buckets. k_decode_finish masks the leaves of proofs that are not pending.
 template <int JOB>
-__global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b) {
-  const int G = (b.npad + 63) / 64;
-  const int blk = JOB < 0 ? (int)blockIdx.x : JOB == 0 ? (int)blockIdx.x : JOB == 1 ? G + (int)blockIdx.x : 3 * G + (int)blockIdx.x;
-  const int job = JOB >= 0 ? JOB : blk < G ? 0 : blk < 3 * G ? 1 : 2;  // 0 GLV A, 1 subgroup, 2 B (wave-uniform)
-  const int role = job == 0 ? 0 : job == 2 ? 2 : ((blk - G) & 1);  // 0 A, 1 C, 2 B
-  const int grp = job == 0 ? blk : job == 2 ? blk - 3 * G : (blk - G) >> 1;
+__global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b, int cglv) {
+  const int G = (b.npad + 63) / 64, nglv = cglv ? 2 * G : G;
+  const int blk = JOB < 0 ? (int)blockIdx.x : JOB == 0 ? (int)blockIdx.x : JOB == 1 ? nglv + (int)blockIdx.x
+                                                                                     : nglv + 2 * G + (int)blockIdx.x;
+  // 0 GLV (A, or C from block G on), 1 subgroup, 2 B (wave-uniform)
+  const int job = JOB >= 0 ? JOB : blk < nglv ? 0 : blk < nglv + 2 * G ? 1 : 2;
+  const int role = job == 0 ? (blk < G ? 0 : 1) : job == 2 ? 2 : ((blk - nglv) & 1);  // 0 A, 1 C, 2 B
+  const int grp = job == 0 ? (blk < G ? blk : blk - G) : job == 2 ? blk - nglv - 2 * G : (blk - nglv) >> 1;
   const int i = grp * 64 + (threadIdx.x & 63);
   if (i >= b.npad) return;
   if (job == 2) {
@@ -74,6 +80,12 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_points(BatchBufs b
   }
   uint64_t ra = 0, rb = 0;
   if (ok) batch_scalar_ab(b.r + (size_t)i * 16, &ra, &rb);
+  if (role == 1) {  // r_i C_i -> the C-sum tree leaf of the proof's key
+    const int kind = i < b.n ? b.kinds[i] : 0;
+    const G1J o = ok ? ZG_DEC_GLV(p, ra, rb) : jac_infinity<Fq>();
+    for (int k = 0; k < ZG_NKINDS; k++) b.ctree[((size_t)b.npad + i) * ZG_NKINDS + k] = k == kind ? o : jac_infinity<Fq>();
+    return;
+  }
   G1A o;
   o.inf = true;
   if (ok) o = jac_to_aff(ZG_DEC_GLV(p, ra, rb));
@@ -106,6 +118,9 @@ __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
   }
   const bool pend = live && st == ST_PENDING;
   if (!pend) b.ptA[i].inf = true;
+  // the C-sum leaves (small shards: r_i C_i from k_decode_points; bisection rewrites them anyway)
+  if (!pend)
+    for (int kd = 0; kd < ZG_NKINDS; kd++) b.ctree[(size_t)leaf * ZG_NKINDS + kd] = jac_infinity<Fq>();
   // B still owes its subgroup check (k_batch_lines) if Proof::read got that far
   b.ptB[i].inf = !(live && (st == ST_PENDING || st == ST_MALFORMED_VK));
   for (int kd = 0; kd < ZG_NKINDS; kd++) {

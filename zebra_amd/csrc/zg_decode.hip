@@ -14,15 +14,16 @@
 namespace zg {
 
 // G1 square roots, then the point jobs (GLV r_i A_i, subgroup checks, B), then per-proof statuses and Fr leaves
-hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b) {
+hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv) {
   hipLaunchKernelGGL(k_decode_sqrt, dim3(2 * groups), dim3(64), 0, st, b);
   static const int split = getenv("ZG_DECODE_SPLIT") ? atoi(getenv("ZG_DECODE_SPLIT")) : 0;
+  const unsigned nglv = cglv ? 2 * groups : groups;
   if (split) {
-    hipLaunchKernelGGL(k_decode_points<0>, dim3(groups), dim3(64), 0, st, b);
-    hipLaunchKernelGGL(k_decode_points<1>, dim3(2 * groups), dim3(64), 0, st, b);
-    hipLaunchKernelGGL(k_decode_points<2>, dim3(groups), dim3(64), 0, st, b);
+    hipLaunchKernelGGL(k_decode_points<0>, dim3(nglv), dim3(64), 0, st, b, cglv);
+    hipLaunchKernelGGL(k_decode_points<1>, dim3(2 * groups), dim3(64), 0, st, b, cglv);
+    hipLaunchKernelGGL(k_decode_points<2>, dim3(groups), dim3(64), 0, st, b, cglv);
   } else {
-    hipLaunchKernelGGL(k_decode_points<-1>, dim3(4 * groups), dim3(64), 0, st, b);
+    hipLaunchKernelGGL(k_decode_points<-1>, dim3(nglv + 3 * groups), dim3(64), 0, st, b, cglv);
   }
   hipLaunchKernelGGL(k_decode_finish, dim3(groups), dim3(64), 0, st, b);
   return hipGetLastError();

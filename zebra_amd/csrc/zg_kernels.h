@@ -103,6 +103,7 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
       b.status[proof] = ST_DECODE_INVALID;
       const int leaf = b.npad + proof, kind = b.kinds[proof];
       for (int m = 0; m < ZG_MAX_IC; m++) b.stree[(leaf * ZG_NKINDS + kind) * ZG_MAX_IC + m] = fp_zero<FrM>();
+      b.ctree[(size_t)leaf * ZG_NKINDS + kind] = jac_infinity<Fq>();  // small shards' C-sum leaf
     }
   }
 }
@@ -371,7 +372,8 @@ __global__ void __launch_bounds__(64) k_tree_f_coop(BatchBufs b, int lo) {
   coop_store(&ws, 0, b.ftree[node]);
 }
 
-// C-sum and Fr scalar-sum tree levels (bisection only: a valid batch's root sums come from K4):
+// C-sum and Fr scalar-sum tree levels (bisection; small shards also build the C levels for the root,
+// ZG_K4_MIN, with the leaves from k_decode_points; otherwise a valid batch's root sums come from K4):
 // the Fr level is cheap and all the node MSM needs; the C level (Jacobian additions) only feeds
 // the delta pairs, so it is built on the side stream concurrently with the node MSM.
 __global__ void __launch_bounds__(64) k_tree_s(BatchBufs b, int lo) {
@@ -383,7 +385,8 @@ __global__ void __launch_bounds__(64) k_tree_s(BatchBufs b, int lo) {
       b.stree[(node * ZG_NKINDS + k) * ZG_MAX_IC + m] =
           fr_add(b.stree[(l * ZG_NKINDS + k) * ZG_MAX_IC + m], b.stree[(r * ZG_NKINDS + k) * ZG_MAX_IC + m]);
 }
-__global__ void __launch_bounds__(64) k_tree_c(BatchBufs b, int lo) {
+__global__ void __launch_bounds__(64) k_tree_c(BatchBufs b, int lo, const int* gate) {
+  if (gate && *gate == 0) return;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= lo * ZG_NKINDS) return;
   const int node = lo + j / ZG_NKINDS, k = j % ZG_NKINDS;

@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(64, WPE) k_batch_lines_lane(BatchBufs b, Fq2* 
       b.status[proof] = ST_DECODE_INVALID;
       const int leaf = b.npad + proof, kind = b.kinds[proof];
       for (int m = 0; m < ZG_MAX_IC; m++) b.stree[(leaf * ZG_NKINDS + kind) * ZG_MAX_IC + m] = fp_zero<FrM>();
+      b.ctree[(size_t)leaf * ZG_NKINDS + kind] = jac_infinity<Fq>();  // small shards' C-sum leaf
     }
   }
 }

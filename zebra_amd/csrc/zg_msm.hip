@@ -270,9 +270,16 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
 
 // the batch root's C sums (ctree node 1) and Fr sums (stree node 1) from the decoded batch;
 // gate: null = always, else only if *gate != 0 (the recompute after a deferred B failure)
+// k4 = 0 (small shards): only the root Fr sums; the C sums are the tree levels of the GLV leaves
 hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate, hipEvent_t bucket0,
-                           hipEvent_t bucket1) {
+                           hipEvent_t bucket1, int k4) {
   m.s = msm_shape(b.npad);
+  if (!k4) {
+    const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;
+    hipLaunchKernelGGL(k_fr_root, dim3(nchunks), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, gate);
+    hipLaunchKernelGGL(k_fr_final, dim3(1), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, nchunks, gate);
+    return hipGetLastError();
+  }
   const unsigned pts = (unsigned)((2 * (size_t)b.npad + 63) / 64);
   hipError_t e = hipMemsetAsync(m.count, 0, sizeof(int) * m.s.ncount(), st);
   if (e != hipSuccess) return e;

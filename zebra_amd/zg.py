@@ -297,7 +297,8 @@ class Context:
         return list(a)
 
     STAT_NAMES = ("batches", "fused_launches", "fused_wait_failures", "b_subgroup_recomputes", "bisections",
-                  "bisect_nodes", "k4_entries", "quad_fchain_launches", "pghr13_calls", "pghr13_batch_failures")
+                  "bisect_nodes", "k4_entries", "quad_fchain_launches", "pghr13_calls", "pghr13_batch_failures",
+                  "glv_csum_batches")
 
     def stats(self):
         """cumulative counters (include/zg.h zg_stats) as a dict"""
