@@ -30,6 +30,10 @@ using namespace zg;
 #define ZG_NTIMINGS 9
 #define ZG_NSTATS 11
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
+#define ZG_TREE_COOP_BELOW_INFLIGHT 64  // ... when other batches are in flight: a lane-per-node level holds a
+                                        // few waves for ~54 serial Fq products, a coop level one wave per
+                                        // node (8k shards, 6 in flight: the coop levels were ~4.5% of a
+                                        // batch's wave-time); the latency it adds is hidden by the pipeline
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
 #define ZG_K4_MIN 16384          // shards from this many (padded) proofs sum r_i C_i by K4's Pippenger buckets;
                                  // below, the GLV products in decode + the C tree levels (8k: K4's bucket grid
@@ -157,6 +161,7 @@ struct zg_ctx {
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
+  int coop_below_env = 0;                  // ... and then applies in flight too
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
   // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
@@ -277,7 +282,10 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
-  if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
+  if (const char* e = getenv("ZG_TREE_COOP_BELOW")) {
+    ctx->coop_below = (size_t)atol(e);
+    ctx->coop_below_env = 1;
+  }
   if (const char* e = getenv("ZG_DEBUG_EACH")) ctx->debug_each = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
@@ -787,8 +795,11 @@ static int run_pipeline(zg_ctx* ctx) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  const size_t coop_below = ctx->coop_below_env || ctx->dev->inflight.load(std::memory_order_relaxed) == 0
+                               ? ctx->coop_below
+                               : std::min(ctx->coop_below, (size_t)ZG_TREE_COOP_BELOW_INFLIGHT);
   for (size_t lo = ctx->npad / (quads ? 8 : 4); lo >= 1; lo /= 2) {
-    if (lo >= ctx->coop_below)
+    if (lo >= coop_below)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
       hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
