@@ -48,6 +48,13 @@ for s in $STEPS; do
     # the driver's default bench line incl. config 2 / config 4 side lines (no CPU leg)
     timeout -k 10 400 python3 -u bench.py --no-cpu > $O/bench_configs.json 2> $O/bench_configs.err || { echo "bench configs failed"; tail -30 $O/bench_configs.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_configs.json')); print({k: d[k] for k in d if 'config' in k.lower() or k in ('value','ms_per_step')})" ;;
+  env8k)
+    # 8k-shard bench (6 in flight) under alternative knobs: ENVS="A=1,B=2 C=3 ..." (comma = same run)
+    for cfg in default ${ENVS:-}; do
+      envs=""; [ "$cfg" != default ] && envs=$(echo $cfg | tr ',' ' ')
+      env $envs timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 40 > $O/b8k_$cfg.json 2> $O/b8k_$cfg.err || { echo "bench 8k $cfg failed"; tail -20 $O/b8k_$cfg.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/b8k_$cfg.json')); print('8k $cfg', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')"
+    done ;;
   quick)
     timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_quick.json 2> $O/bench_quick.err || { echo "bench quick failed"; tail -30 $O/bench_quick.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_quick.json')); print('64k', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"

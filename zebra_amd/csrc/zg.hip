@@ -160,6 +160,8 @@ struct zg_ctx {
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
+  int singles = -1;          // ZG_FCHAIN_SINGLE: -1 auto (a fused launch runs one proof per f-chain lane), 0 never
+  int singles_last = 0;      // the last batch's f-chain wrote the per-proof leaves (bisection reuses them)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
   int coop_below_env = 0;                  // ... and then applies in flight too
   hipEvent_t ev[ZG_NEV] = {};
@@ -281,6 +283,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
+  if (const char* e = getenv("ZG_FCHAIN_SINGLE")) ctx->singles = atoi(e);
   if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
   if (const char* e = getenv("ZG_TREE_COOP_BELOW")) {
     ctx->coop_below = (size_t)atol(e);
@@ -699,7 +702,8 @@ hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchB
 hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
 hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines);
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
-                                    int* fail);
+                                    int* fail, int per);
+hipError_t launch_prog_fchain1(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
 hipError_t launch_jj_comb(hipStream_t st, uint32_t* table);                                    // zg_jubjub.hip
 hipError_t launch_redjubjub(hipStream_t st, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                             const uint8_t* gen, int n, const uint32_t* comb, uint8_t* ok);
@@ -765,6 +769,10 @@ static int run_pipeline(zg_ctx* ctx) {
                      (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu &&
                       ctx->dev->inflight.load(std::memory_order_relaxed) == 0);
   ctx->fused_last = fused;
+  // a fused (lone, small) batch is latency-bound: one proof per f-chain lane, 4 rounds per step
+  // instead of the pair step's 6 (config 2: the fused launch 2.95 ms with pairs, r03v)
+  const bool singles = fused && ctx->singles != 0;
+  ctx->singles_last = singles;
   // four proofs per lane on large shards (one block per CU from 64k proofs on): 64 Fq2 products
   // per four proofs and step instead of 76 (k_batch_fchain4)
   const bool quads = !fused && ctx->npad >= 4 && (ctx->quads == 1 || (ctx->quads < 0 && ctx->npad >= ZG_QUAD_MIN));
@@ -772,9 +780,15 @@ static int run_pipeline(zg_ctx* ctx) {
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
-    HIPCHK(launch_prog_lines_fchain(groups + pgroups, ctx->stream, b, ctx->d_lines, ctx->d_prog, b.bfail + 1));
-    // no-op unless bfail / wait failure
-    HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)b.bfail));
+    if (singles) {
+      HIPCHK(launch_prog_lines_fchain(2 * groups, ctx->stream, b, ctx->d_lines, ctx->d_prog, b.bfail + 1, 1));
+      // no-op unless bfail / wait failure
+      HIPCHK(launch_prog_fchain1(groups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)b.bfail));
+    } else {
+      HIPCHK(launch_prog_lines_fchain(groups + pgroups, ctx->stream, b, ctx->d_lines, ctx->d_prog, b.bfail + 1, 2));
+      // no-op unless bfail / wait failure
+      HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)b.bfail));
+    }
   } else {
     const bool lane = ctx->lines_lane > 0 || (ctx->lines_lane < 0 && ctx->npad >= ZG_LINES_LANE_MIN);
     if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
@@ -798,7 +812,7 @@ static int run_pipeline(zg_ctx* ctx) {
   const size_t coop_below = ctx->coop_below_env || ctx->dev->inflight.load(std::memory_order_relaxed) == 0
                                ? ctx->coop_below
                                : std::min(ctx->coop_below, (size_t)ZG_TREE_COOP_BELOW_INFLIGHT);
-  for (size_t lo = ctx->npad / (quads ? 8 : 4); lo >= 1; lo /= 2) {
+  for (size_t lo = ctx->npad / (singles ? 2 : quads ? 8 : 4); lo >= 1; lo /= 2) {
     if (lo >= coop_below)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
@@ -928,7 +942,7 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
       HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
       bool leaves = false;
       for (int q = 0; q < m; q++) leaves = leaves || nodes[off + q] >= (int)ctx->npad;
-      if (leaves) {  // per-proof Miller leaves exist only on demand (the f-chain writes pair nodes)
+      if (leaves && !ctx->singles_last) {  // per-proof Miller leaves on demand (unless the f-chain wrote them)
         HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
         HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
         HIPCHK(launch_prog_leaf_fchain(nblocks(m), ctx->side, b, (const Fq2*)ctx->d_lines, (const int*)ctx->d_nodes, m));
@@ -945,7 +959,7 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
                          ctx->stream, b, nb,
                          (const int*)nullptr);
       HIPCHK(hipGetLastError());
-      if (leaves) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[11], 0));
+      if (leaves && !ctx->singles_last) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[11], 0));
     }
     hipLaunchKernelGGL(k_node_final, dim3(m), dim3(64), 0, ctx->stream, b, nb, mode);
     HIPCHK(hipGetLastError());

@@ -198,7 +198,80 @@ __device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines
     reinterpret_cast<Fq2*>(&b.ftree[b.npad / 2 + pair])[wave] = v;
   }
 }
+// One proof per lane (small lone batches: config 2, bisection-heavy config 4): the single-proof
+// programs MSQ / M (25 Fq2 products in 4 rounds per step against the pair step's 38 in 6), so a
+// step's latency -- what a few-block batch pays 68 times -- is two thirds of the pair step's. The
+// Miller values are the leaves ftree[npad + i]; the product tree starts one level lower. prog / fail
+// as fchain_body: in the fused launch block blk waits for lines block blk (its own 64 proofs).
+__device__ __forceinline__ void fchain1_body(const BatchBufs& b, const Fq2* lines, int blk, const AtomSpace& at,
+                                             const int* prog, int* fail) {
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int proof = blk * 64 + lane;
+  const bool inb = proof < b.npad;
+  const bool act = inb && proof_active(b, proof);
+  static_assert(ZG_FC_NW == 8, "waves 0..5 carry f, waves 6, 7 load the line");
+  int seen = 0;
+  auto wait_lines = [&](int n) {
+    if (!prog || n < seen) return;
+    for (uint32_t it = 0;; it++) {
+      const int d = wave_uniform(__hip_atomic_load(&prog[blk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (d > n) {
+        seen = d;
+        break;
+      }
+      if (wave_uniform(__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+      if (it >= (1u << 19)) {
+        __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  };
+  auto load_lines = [&](int n) {
+    wait_lines(n);
+    const Fq2* src = lines + ((size_t)n * b.npad + (inb ? proof : 0)) * 3;
+    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? src[j] : (j == 0 ? f2_one() : f2_zero()));
+  };
+  if (wave < 6)
+    at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  else
+    load_lines(0);
+  __syncthreads();
+  int n = 0;
+  for (int i = ZG_XH_TOP;; i--) {
+    const bool last = i < 0;
+    const bool addbit = !last && ((ZG_XH >> i) & 1ull);
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
+      prog_run<false>(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      __syncthreads();
+      n++;
+      if (wave < 6)
+        at.put(wave, v);
+      else if (n < ZG_NCOEFF)
+        load_lines(n);
+      __syncthreads();
+    }
+    if (last) break;
+  }
+  if (wave < 6 && inb) {
+    Fq2 v = at.get(wave);
+    if (wave >= 3) v = f2_neg(v);  // conjugate (u < 0)
+    reinterpret_cast<Fq2*>(&b.ftree[b.npad + proof])[wave] = v;
+  }
+}
+
 // gate (optional): {bfail, fused-wait failure}; the launch is a no-op unless one is set
+#if defined(ZG_TU_PROG_FCHAIN)
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain1(BatchBufs b, const Fq2* lines, const int* gate) {
+  if (gate && gate[0] == 0 && gate[1] == 0) return;
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  fchain1_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, nullptr, nullptr);
+}
+#endif
 #if defined(ZG_TU_PROG_FCHAIN)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, const Fq2* lines, const int* gate) {
   if (gate && gate[0] == 0 && gate[1] == 0) return;
@@ -277,12 +350,15 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, co
 // dispatched first, so the consumers' waits end. proof_active may still see a B that the
 // lines blocks reject (G2 subgroup) as active: bfail then gates the k_batch_fchain re-run.
 #if defined(ZG_TU_PROG_FUSED)
+template <int PER>
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_lines_fchain(BatchBufs b, Fq2* lines, int* prog, int* fail) {
   static_assert(ZG_FCHAIN_SLOTS >= ZG_LINES_SLOTS && ZG_FC_NW >= ZG_LINES_NW, "fused block covers both");
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
   const int P = (b.npad + 63) / 64;
   if ((int)blockIdx.x < P)
     lines_body(b, lines, blockIdx.x, AtomSpace{lds_atoms}, prog);
+  else if (PER == 1)
+    fchain1_body(b, lines, blockIdx.x - P, AtomSpace{lds_atoms}, prog, fail);
   else
     fchain_body(b, lines, blockIdx.x - P, AtomSpace{lds_atoms}, prog, fail);
 }

@@ -15,5 +15,11 @@ hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& 
   hipLaunchKernelGGL(k_batch_fchain, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines, gate);
   return hipGetLastError();
 }
+// one proof per lane (the leaves): the gated re-run of the fused single-proof launch
+hipError_t launch_prog_fchain1(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines,
+                               const int* gate) {
+  hipLaunchKernelGGL(k_batch_fchain1, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines, gate);
+  return hipGetLastError();
+}
 
 }  // namespace zg

@@ -10,9 +10,13 @@
 
 namespace zg {
 
+// per: proofs per f-chain lane (1: MSQ / M programs, leaves; 2: pair nodes)
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
-                                    int* fail) {
-  hipLaunchKernelGGL(k_lines_fchain, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines, prog, fail);
+                                    int* fail, int per) {
+  if (per == 1)
+    hipLaunchKernelGGL(k_lines_fchain<1>, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines, prog, fail);
+  else
+    hipLaunchKernelGGL(k_lines_fchain<2>, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines, prog, fail);
   return hipGetLastError();
 }
 
