@@ -103,13 +103,23 @@ __global__ void __launch_bounds__(ZG_MSM_BT) k_msm_bucket(BatchBufs b, MsmBufs m
     const int lo = m.start[bucket], len = m.start[bucket + 1] - lo;
     const int beg = lo + len * part / P, end = lo + len * (part + 1) / P;
     const Fq beta = fq_const(G1_BETA);
+    // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
+    // status between count and scatter -- then bfail > 0 and the gated recompute redoes it; it
+    // must still stay inside the buffers). The next entry's point is gathered while the current
+    // one is added (software pipelining: its L2 / HBM latency hides behind the addition).
+    auto gather = [&](int e, uint32_t* ent, G1A* c) {
+      *ent = m.entries[e];
+      const uint32_t pi = *ent >> 2;
+      *c = b.ptAC[(size_t)b.npad + (pi < (uint32_t)b.npad ? pi : 0)];
+    };
+    uint32_t ent_n = 0;
+    G1A c_n;
+    if (beg < end) gather(beg, &ent_n, &c_n);
     for (int e = beg; e < end; e++) {
-      const uint32_t ent = m.entries[e];
-      // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
-      // status between count and scatter -- then bfail > 0 and the gated recompute redoes it;
-      // it must still stay inside the buffers)
+      const uint32_t ent = ent_n;
+      const G1A c = c_n;
+      if (e + 1 < end) gather(e + 1, &ent_n, &c_n);
       if ((ent >> 2) >= (uint32_t)b.npad) continue;
-      const G1A c = b.ptAC[(size_t)b.npad + (ent >> 2)];
       const Fq x = (ent & 2u) ? fq_mul(c.x, beta) : c.x;
       const Fq y = (ent & 1u) ? fq_neg(c.y) : c.y;
       acc = jac_add_aff_inl(acc, G1A{x, y, false});
