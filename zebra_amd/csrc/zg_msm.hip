@@ -285,6 +285,9 @@ hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const 
                            hipEvent_t bucket1, int k4) {
   m.s = msm_shape(b.npad);
   if (!k4) {
+    hipError_t e;  // the bucket-phase events still bracket something (an empty phase): callers time them
+    if (bucket0 && (e = hipEventRecord(bucket0, st)) != hipSuccess) return e;
+    if (bucket1 && (e = hipEventRecord(bucket1, st)) != hipSuccess) return e;
     const int nchunks = (b.npad + ZG_FR_CHUNK - 1) / ZG_FR_CHUNK;
     hipLaunchKernelGGL(k_fr_root, dim3(nchunks), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, gate);
     hipLaunchKernelGGL(k_fr_final, dim3(1), dim3(ZG_NKINDS * ZG_MAX_IC * ZG_FR_G), 0, st, b, m, nchunks, gate);
