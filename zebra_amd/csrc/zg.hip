@@ -30,14 +30,10 @@ using namespace zg;
 #define ZG_NTIMINGS 9
 #define ZG_NSTATS 11
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
-#define ZG_TREE_COOP_BELOW_INFLIGHT 64  // ... when other batches are in flight: a lane-per-node level holds a
-                                        // few waves for ~54 serial Fq products, a coop level one wave per
-                                        // node (8k shards, 6 in flight: the coop levels were ~4.5% of a
-                                        // batch's wave-time); the latency it adds is hidden by the pipeline
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
-#define ZG_K4_MIN 16384          // shards from this many (padded) proofs sum r_i C_i by K4's Pippenger buckets;
-                                 // below, the GLV products in decode + the C tree levels (8k: K4's bucket grid
-                                 // held 17% of a batch's wave-time for ~1 ms of lone-lane addition chains)
+#define ZG_K4_MIN 16384          // lone batches from this many (padded) proofs sum r_i C_i by K4's Pippenger
+                                 // buckets; smaller lone batches by the GLV products in decode + the C tree
+                                 // levels (run_pipeline: batches in flight always use K4)
 #define ZG_LINES_LANE_MIN 32768  // straight-line R-chain from here (r03: 64k 14.93 -> 14.47 ms per batch in
                                  // flight; 16k 4.90 -> 5.14 and 8k 3.21 -> 3.63 favour the staged program)
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
@@ -163,7 +159,6 @@ struct zg_ctx {
   int singles = -1;          // ZG_FCHAIN_SINGLE: -1 auto (a fused launch runs one proof per f-chain lane), 0 never
   int singles_last = 0;      // the last batch's f-chain wrote the per-proof leaves (bisection reuses them)
   size_t coop_below = ZG_TREE_COOP_BELOW;  // ZG_TREE_COOP_BELOW overrides (product-tree wave-per-node levels)
-  int coop_below_env = 0;                  // ... and then applies in flight too
   hipEvent_t ev[ZG_NEV] = {};
   float timings[ZG_NTIMINGS] = {};
   // [0] batches, [1] fused launches, [2] fused-wait failures, [3] B subgroup failures
@@ -285,10 +280,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_FCHAIN_SINGLE")) ctx->singles = atoi(e);
   if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
-  if (const char* e = getenv("ZG_TREE_COOP_BELOW")) {
-    ctx->coop_below = (size_t)atol(e);
-    ctx->coop_below_env = 1;
-  }
+  if (const char* e = getenv("ZG_TREE_COOP_BELOW")) ctx->coop_below = (size_t)atol(e);
   if (const char* e = getenv("ZG_DEBUG_EACH")) ctx->debug_each = atoi(e);
   hipError_t e = hipSetDevice(ctx->device);
   auto A = [&](hipError_t r) {
@@ -735,7 +727,13 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipMemsetAsync(b.bfail, 0, 2 * sizeof(int), ctx->stream));  // bfail, fused-wait failure
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
-  const int k4 = (long)ctx->npad >= ctx->k4_min ? 1 : 0;
+  // a lone small batch is latency-bound: the GLV products ride on decode and the tree replaces K4's
+  // chains of lone-lane additions (config 2 7.18 -> 6.24 ms with the single-proof f-chain, config 4
+  // 25.3 -> 20.7 ms: bisection reuses the tree). With other batches in flight the device is
+  // issue-bound and K4's few, mostly waiting waves cost less than the GLV products' work (8k shards,
+  // 6 in flight: 2.74 ms per batch with K4, 2.96 with the GLV path; profiles/r04h_env8k.txt)
+  const bool alone = ctx->dev->inflight.load(std::memory_order_relaxed) == 0;
+  const int k4 = (long)ctx->npad >= ctx->k4_min || !alone ? 1 : 0;
   ctx->k4_last = k4;
   HIPCHK(launch_batch_decode(dgroups, ctx->stream, b, !k4));
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -809,11 +807,8 @@ static int run_pipeline(zg_ctx* ctx) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  const size_t coop_below = ctx->coop_below_env || ctx->dev->inflight.load(std::memory_order_relaxed) == 0
-                               ? ctx->coop_below
-                               : std::min(ctx->coop_below, (size_t)ZG_TREE_COOP_BELOW_INFLIGHT);
   for (size_t lo = ctx->npad / (singles ? 2 : quads ? 8 : 4); lo >= 1; lo /= 2) {
-    if (lo >= coop_below)
+    if (lo >= ctx->coop_below)
       hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
     else
       hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
