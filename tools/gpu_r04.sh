@@ -55,6 +55,22 @@ for s in $STEPS; do
       env $envs timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 40 > $O/b8k_$cfg.json 2> $O/b8k_$cfg.err || { echo "bench 8k $cfg failed"; tail -20 $O/b8k_$cfg.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/b8k_$cfg.json')); print('8k $cfg', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')"
     done ;;
+  inflight8k)
+    # 8k shards at several batches-in-flight depths
+    for inf in ${DEPTHS:-4 6 8 10}; do
+      timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs 8192 --inflight $inf --steps 40 > $O/b8k_if$inf.json 2> $O/b8k_if$inf.err || { echo "bench 8k inflight $inf failed"; tail -20 $O/b8k_if$inf.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/b8k_if$inf.json')); print('8k inflight $inf', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')"
+    done ;;
+  pmcsize)
+    # VALU instructions per batch by kernel, 64k (4 in flight) and 8k (6 in flight), one --pmc pass each
+    cd /tmp && export TMPDIR=/tmp
+    for cfg in "65536 4 8" "8192 6 36"; do
+      set -- $cfg
+      timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $O/pmc_$1 -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs $1 --inflight $2 --steps $3 --warmup 0 > $O/pmc_$1.out 2> $O/pmc_$1.err || { echo "pmc $1 failed"; tail -5 $O/pmc_$1.err; exit 1; }
+      # batches verified = timed steps + the warmup-free pipeline's own checks (steps + inflight drained)
+      python3 $R/tools/pmc_per_batch.py $O/pmc_$1 $3 > $O/pmc_per_batch_$1.txt && head -16 $O/pmc_per_batch_$1.txt
+    done
+    cd $R ;;
   quick)
     timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs > $O/bench_quick.json 2> $O/bench_quick.err || { echo "bench quick failed"; tail -30 $O/bench_quick.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_quick.json')); print('64k', d['value'], d['ms_per_step'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['phase_ms'].items()})"
