@@ -91,7 +91,11 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint32_t*)lines, nl * 24);
   hipLaunchKernelGGL(k_init, dim3((n + 255) / 256), dim3(256), 0, 0, status, ptA, n);
   CK(hipMemset(ftree, 0, sizeof(Fq12) * 2 * npad));
+  int* bfail;
+  CK(hipMalloc(&bfail, 8));
+  CK(hipMemset(bfail, 0, 8));
   BatchBufs b{};
+  b.bfail = bfail;
   b.status = status;
   b.ptA = ptA;
   b.ftree = ftree;
@@ -119,6 +123,9 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(h.data(), ftree + npad / 4, h.size() * 4, hipMemcpyDeviceToHost));
   uint64_t hash = 0xcbf29ce484222325ull;
   for (uint32_t w : h) hash = (hash ^ w) * 0x100000001b3ull;
+  int hf[2];
+  CK(hipMemcpy(hf, bfail, 8, hipMemcpyDeviceToHost));
+  if (hf[1]) printf("dataflow wait gave up (bfail[1] = %d)\n", hf[1]);
   const double macs = 5192.0 * 288.0 * n;
   printf("fchain4 n=%d blocks=%u: best %.3f ms, mean %.3f ms, %.2f T alg-MAC/s, nodes hash %016llx\n", n, blocks, best,
          sum / reps, macs / (best * 1e-3) / 1e12, (unsigned long long)hash);
