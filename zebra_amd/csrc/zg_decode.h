@@ -34,7 +34,11 @@ namespace zg {
 // The heavy waves are dispatched first, two per SIMD (ZG_DECODE_WPE), and the B waves fill the
 // tail. The scalar products run before the statuses are known (a point that did not decode
 // skips its own; the rest are masked by k_decode_finish).
-__global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) {
+#if defined(ZG_TU_DECODE_SQRT)  // zg_decode_sqrt.hip: every callee inlined, no call frames
+#ifndef ZG_DECODE_SQRT_WPE
+#define ZG_DECODE_SQRT_WPE ZG_DECODE_WPE
+#endif
+__global__ void __launch_bounds__(64, ZG_DECODE_SQRT_WPE) k_decode_sqrt(BatchBufs b) {
   const int role = blockIdx.x & 1;  // 0 A, 1 C (wave-uniform)
   const int i = (blockIdx.x >> 1) * 64 + (threadIdx.x & 63);
   if (i >= b.npad) return;
@@ -44,6 +48,7 @@ __global__ void __launch_bounds__(64, ZG_DECODE_WPE) k_decode_sqrt(BatchBufs b) 
     p.inf = true;
   b.ptAC[(size_t)role * b.npad + i] = p;
 }
+#else
 
 // JOB < 0: every job in one launch (grid 4G); JOB = 0 / 1 / 2: that job alone (grid G / 2G / G,
 // ZG_DECODE_SPLIT=1: separate launches, so each job gets its own register budget and its own
@@ -136,5 +141,7 @@ __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
     for (int j = 0; j < kk; j++) s[1 + j] = fr_mul(rf, fr_to_mont(x[j]));
   }
 }
+
+#endif  // ZG_TU_DECODE_SQRT
 
 }  // namespace zg

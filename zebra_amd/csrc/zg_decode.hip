@@ -13,9 +13,11 @@
 
 namespace zg {
 
+hipError_t launch_decode_sqrt(unsigned groups, hipStream_t st, const BatchBufs& b);  // zg_decode_sqrt.hip
+
 // G1 square roots, then the point jobs (GLV r_i A_i, subgroup checks, B), then per-proof statuses and Fr leaves
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv) {
-  hipLaunchKernelGGL(k_decode_sqrt, dim3(2 * groups), dim3(64), 0, st, b);
+  launch_decode_sqrt(groups, st, b);
   static const int split = getenv("ZG_DECODE_SPLIT") ? atoi(getenv("ZG_DECODE_SPLIT")) : 0;
   const unsigned nglv = cglv ? 2 * groups : groups;
   if (split) {

@@ -18,7 +18,15 @@
 
 #define ZG_HD __host__ __device__
 #define ZG_INL __host__ __device__ __forceinline__
+// ZG_INLINE_ALL (a translation unit that defines it before any zebra header): every ZG_NOINL
+// function is inlined into the unit's kernels -- no call frames, so no private segment for a kernel
+// whose whole call tree fits its register budget (zg_decode_sqrt.hip)
+#ifdef ZG_INLINE_ALL
+#define ZG_NOINL __host__ __device__ __forceinline__
+#else
 #define ZG_NOINL __host__ __device__ __attribute__((noinline))
+#endif
+#define ZG_POW_FN ZG_NOINL inline
 
 // ZG_FQ29 (default): Fq products in 29-bit digits (zg_fq29.h / gen_fq29.py); 0: the 32-bit-word
 // FIPS asm (zg_fips.h) on the device
@@ -428,12 +436,81 @@ ZG_NOINL inline Fq fq_inv_vartime(Fq a) {
 // constant-time Fermat inverse (kept for reference / tests)
 ZG_INL Fq fq_inv_fermat(const Fq& a) { return fq_pow_limbs(a, FQ_EXP_INV, 381); }
 
-// a^((p-3)/4) by the sliding-window chain of zg_constants.h (w = 5: 16 odd powers,
-// 375 squarings + 67 multiplications, vs 379 + 228 for square-and-multiply).
-ZG_NOINL inline void fq_pow_pm3_4_p(Fq* out, const Fq* ap) {
-#if ZG_FQ29
-  // digit-resident chain (Montgomery R' = 2^406, zg_fq29_gen.h fq29d_*): the 375 squarings and 82
-  // multiplications split, repack and canonicalise nothing; one conversion in, one out
+// a^((p-3)/4) by a sliding-window chain of zg_constants.h.
+#ifndef ZG_SQRT_W
+#define ZG_SQRT_W 4
+#endif
+#if ZG_FQ29 && (ZG_SQRT_W == 3 || ZG_SQRT_W == 4)
+// w = 4 (375 squarings + 79 multiplications, 8 odd powers) or w = 3 (377 + 106, 4 odd powers): the
+// chain is the same for every lane, so the table index is wave-uniform and a switch on it reads
+// fixed registers -- the table stays in VGPRs (112 or 56) instead of the private segment a
+// runtime-indexed array needs.
+#if ZG_SQRT_W == 4
+#define ZG_SQ_CHAIN FQ_PM3_4_CHAIN4
+#define ZG_SQ_CHAIN_LEN FQ_PM3_4_CHAIN4_LEN
+#else
+#define ZG_SQ_CHAIN FQ_PM3_4_CHAIN3
+#define ZG_SQ_CHAIN_LEN FQ_PM3_4_CHAIN3_LEN
+#endif
+struct Fq29D {
+  uint32_t d[14];
+};
+// s = T_k for a wave-uniform k: eight separate values and copies in the arms of a switch, so
+// nothing indexes an array at run time
+ZG_INL void fq29d_pick8(uint32_t* s, const Fq29D& T0, const Fq29D& T1, const Fq29D& T2, const Fq29D& T3,
+                        const Fq29D& T4, const Fq29D& T5, const Fq29D& T6, const Fq29D& T7, int k) {
+  Fq29D v;
+  switch (k) {
+    case 0: v = T0; break;
+    case 1: v = T1; break;
+    case 2: v = T2; break;
+    case 3: v = T3; break;
+    case 4: v = T4; break;
+    case 5: v = T5; break;
+    case 6: v = T6; break;
+    default: v = T7; break;
+  }
+#pragma unroll
+  for (int w = 0; w < 14; w++) s[w] = v.d[w];
+}
+#endif
+ZG_POW_FN void fq_pow_pm3_4_p(Fq* out, const Fq* ap) {
+#if ZG_FQ29 && (ZG_SQRT_W == 3 || ZG_SQRT_W == 4)
+  // digit-resident chain (Montgomery R' = 2^406, zg_fq29_gen.h fq29d_*)
+  Fq29D T0, T1, T2, T3;
+  uint32_t a2[14], r[14], t[14], s[14];
+  fq29d_from_mont(T0.d, ap->l);
+  fq29d_sqr(a2, T0.d);
+  fq29d_mul(T1.d, T0.d, a2);
+  fq29d_mul(T2.d, T1.d, a2);
+  fq29d_mul(T3.d, T2.d, a2);
+#if ZG_SQRT_W == 4
+  Fq29D T4, T5, T6, T7;
+  fq29d_mul(T4.d, T3.d, a2);
+  fq29d_mul(T5.d, T4.d, a2);
+  fq29d_mul(T6.d, T5.d, a2);
+  fq29d_mul(T7.d, T6.d, a2);
+#else
+  const Fq29D &T4 = T3, &T5 = T3, &T6 = T3, &T7 = T3;  // never picked
+#endif
+  fq29d_pick8(r, T0, T1, T2, T3, T4, T5, T6, T7, ZG_SQ_CHAIN[0][1] >> 1);
+  for (int i = 1; i < ZG_SQ_CHAIN_LEN; i++) {
+    for (int q = 0; q < ZG_SQ_CHAIN[i][0]; q++) {
+      fq29d_sqr(t, r);
+#pragma unroll
+      for (int w = 0; w < 14; w++) r[w] = t[w];
+    }
+    const int o = ZG_SQ_CHAIN[i][1];
+    if (o) {
+      fq29d_pick8(s, T0, T1, T2, T3, T4, T5, T6, T7, o >> 1);
+      fq29d_mul(t, r, s);
+#pragma unroll
+      for (int w = 0; w < 14; w++) r[w] = t[w];
+    }
+  }
+  fq29d_to_mont(out->l, r);
+#elif ZG_FQ29
+  // w = 5 (375 squarings + 67 multiplications; 16 odd powers, a runtime-indexed table)
   uint32_t tbl[16][14], a2[14], r[14], t[14];
   fq29d_from_mont(tbl[0], ap->l);
   fq29d_sqr(a2, tbl[0]);
