@@ -14,7 +14,14 @@ namespace zg {
 #endif
 #if ZG_DECODE_FQD
 #define ZG_DEC_SUBGROUP g1_in_subgroup_d
-#define ZG_DEC_GLV g1_glv_mul_w2  // two columns per step (g1_glv_mul_d: one)
+// GLV r_i A_i one column per step (64 doublings + 64 mixed additions of +-P or +-(P + sigma P),
+// operands selected from registers). g1_glv_mul_w2 (two columns per step from an eight-entry
+// per-lane table: 32 additions fewer) is 2.5% faster on the decode kernel but gathers its table
+// entries from the private segment with a different index per lane -- 2.1 GB of HBM traffic per
+// 64k launch against 0.18 GB (profiles/r04p_*, r04o_*)
+#ifndef ZG_DEC_GLV
+#define ZG_DEC_GLV g1_glv_mul_d
+#endif
 #else
 #define ZG_DEC_SUBGROUP g1_in_subgroup
 #define ZG_DEC_GLV g1_glv_mul
@@ -107,13 +114,19 @@ __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
   const int leaf = b.npad + i;
   const int kind = live ? b.kinds[i] : 0;
   uint8_t st = ST_PENDING;
-  Fr x[ZG_MAX_INPUTS];
   int k = 0, kk = 0;
+  // the inputs are read where they are used (canonicity here, the Fr leaves below): no per-lane
+  // array of them, so no private segment
+  const uint8_t* in = b.inputs + (size_t)i * 288;
   if (live) {
     k = b.ninputs ? b.ninputs[i] : KIND_NINPUTS[kind];
     kk = k < ZG_MAX_INPUTS ? k : ZG_MAX_INPUTS;
     const bool ok = b.okbits[3 * i] && b.okbits[3 * i + 1] && b.okbits[3 * i + 2];
-    if (!inputs_canonical(b.inputs + (size_t)i * 288, kk, x))
+    bool canon = true;
+#pragma unroll
+    for (int j = 0; j < ZG_MAX_INPUTS; j++)
+      if (j < kk) canon = canon && fp_lt_modulus<FrM>(fr_limbs_from_le(in + 32 * j));
+    if (!canon)
       st = ST_INPUT_NONCANONICAL;
     else if (!ok)
       st = ST_DECODE_INVALID;
@@ -138,7 +151,9 @@ __global__ void __launch_bounds__(64) k_decode_finish(BatchBufs b) {
     const Fr rf = batch_scalar_fr(ra, rb);
     Fr* s = b.stree + (leaf * ZG_NKINDS + kind) * ZG_MAX_IC;
     s[0] = rf;
-    for (int j = 0; j < kk; j++) s[1 + j] = fr_mul(rf, fr_to_mont(x[j]));
+#pragma unroll
+    for (int j = 0; j < ZG_MAX_INPUTS; j++)
+      if (j < kk) s[1 + j] = fr_mul(rf, fr_to_mont(fr_limbs_from_le(in + 32 * j)));
   }
 }
 
