@@ -92,6 +92,10 @@ int main() {
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   hipMemcpy(c, dc, 8, hipMemcpyDeviceToHost);
-  printf("final_exp: %lld cycles, %.3f ms\n", c[0], ms);
+  Fq12 o[2];
+  hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
+  unsigned long long hsh = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < sizeof(Fq12) / 4; i++) hsh = (hsh ^ ((const uint32_t*)o)[i]) * 0x100000001b3ull;
+  printf("final_exp: %lld cycles, %.3f ms, output hash %016llx\n", c[0], ms, hsh);
   return 0;
 }
