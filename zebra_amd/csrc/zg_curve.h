@@ -307,7 +307,7 @@ ZG_NOINL inline int g1_decompress(const uint8_t* b, G1A* out, bool check_subgrou
 }
 
 // pairing 0.14 G2Compressed::into_affine. 96 bytes: x.c1 (flags) || x.c0.
-ZG_NOINL inline int g2_decompress(const uint8_t* b, G2A* out, bool check_subgroup = true) {
+ZG_DEC_INL inline int g2_decompress(const uint8_t* b, G2A* out, bool check_subgroup = true) {
   uint8_t f = b[0];
   if (!(f & 0x80)) return DEC_ERR;
   if (f & 0x40) {

@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#define ZG_TU_DECODE 1  // ZG_DEC_INL wrappers inline here (zg_field.h)
+#define ZG_SQRT_W 3      // B's inlined square roots: the w = 3 chain's 56-register table fits beside
+                         // f2_sqrt's state (w = 4 spilled 40 VGPRs here; k_decode_sqrt keeps w = 4)
 #include "../../include/zg.h"
 #ifndef ZG_DECODE_WPE
 #define ZG_DECODE_WPE 2

@@ -26,7 +26,15 @@
 #else
 #define ZG_NOINL __host__ __device__ __attribute__((noinline))
 #endif
-#define ZG_POW_FN ZG_NOINL inline
+// ZG_DEC_INL: functions the decode unit (zg_decode.hip, ZG_TU_DECODE) inlines into its kernels -- the
+// point wrappers that take their arguments by pointer / reference and B's square root, whose call
+// frames were that kernel's private segment -- and that stay out of line everywhere else
+#ifdef ZG_TU_DECODE
+#define ZG_DEC_INL __host__ __device__ __forceinline__
+#else
+#define ZG_DEC_INL ZG_NOINL
+#endif
+#define ZG_POW_FN ZG_DEC_INL inline
 
 // ZG_FQ29 (default): Fq products in 29-bit digits (zg_fq29.h / gen_fq29.py); 0: the 32-bit-word
 // FIPS asm (zg_fips.h) on the device

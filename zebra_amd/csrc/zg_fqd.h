@@ -271,7 +271,7 @@ ZG_INL FqD fqd_neg2(const FqD& x) { return fqd_sub<3, 0, 1>(fqd_zero(), x); }
 
 // G1 subgroup check (zg_curve.h g1_in_subgroup, same test): sigma(P) == -[x^2] P with the
 // 127 doublings and 16 mixed additions in FqD
-ZG_NOINL inline bool g1_in_subgroup_d(const G1A& p) {
+ZG_DEC_INL inline bool g1_in_subgroup_d(const G1A& p) {
   if (p.inf) return true;
   const FqD px = fqd_from(p.x), py = fqd_from(p.y);
   G1D q = g1d_from_aff(px, py);

@@ -146,7 +146,7 @@ ZG_INL G1J g1_glv_mul(const G1A& p, uint64_t a, uint64_t b) {
   return r;
 }
 // the same product with the 64 doublings and mixed additions in lazy digits (zg_fqd.h)
-ZG_NOINL inline void g1_glv_mul_d_p(G1J* out, const G1A* pp, uint64_t a, uint64_t b) {
+ZG_DEC_INL inline void g1_glv_mul_d_p(G1J* out, const G1A* pp, uint64_t a, uint64_t b) {
   const FqD px = fqd_from(pp->x), py = fqd_from(pp->y);
   const FqD bx = fqd_mul(px, fqd_from(fq_const(G1_BETA2))), ny = fqd_neg2(py);  // < 2p, < 3p
   uint64_t k1 = b, e = 0;

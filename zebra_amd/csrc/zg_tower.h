@@ -103,10 +103,34 @@ ZG_INL Fq2 f2_pow_limbs(const Fq2& a, const uint32_t* e, int nbits) {
 //   d = (a0 + g)/2 != 0, e = d^((p-3)/4):
 //   d a square:  y = e d + (a1 e / 2) u          ((e d)^2 = d, 1/(e d) = e)
 //   otherwise :  y = a1 e / 2 - (e d) u          (-d is a square; (p-3)/4 is even)
-ZG_NOINL inline bool f2_sqrt(const Fq2& a, Fq2* out) {
-  if (fq_is_zero(a.c1)) {  // a in Fq: sqrt(a0) or sqrt(-a0) u
-    const Fq e = fq_pow_pm3_4(a.c0);  // (-a0)^((p-3)/4) == e too: (p-3)/4 is even
-    const Fq s = fq_mul(e, a.c0);
+ZG_DEC_INL inline bool f2_sqrt(const Fq2& a, Fq2* out) {
+  // one call site of the exponentiation (pass 0: a0, or the norm n; pass 1: d), so a unit that
+  // inlines it (ZG_DEC_INL) holds one copy
+  const bool c1z = fq_is_zero(a.c1);
+  const Fq n = c1z ? a.c0 : fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+  Fq x = n, e0 = n, d = n;
+  bool ok = true;
+  for (int pass = 0; pass < 2; pass++) {
+    const Fq e = fq_pow_pm3_4(x);
+    if (pass == 1) {
+      e0 = e;
+      break;
+    }
+    if (c1z) {  // a in Fq: sqrt(a0) or sqrt(-a0) u; (-a0)^((p-3)/4) == e too: (p-3)/4 is even
+      e0 = e;
+      break;
+    }
+    const Fq g = fq_mul(e, n);
+    if (!fq_eq(fq_sqr(g), n)) {
+      ok = false;
+      break;
+    }
+    d = fq_half(fq_add(a.c0, g));
+    x = d;
+  }
+  if (!ok) return false;
+  if (c1z) {
+    const Fq s = fq_mul(e0, a.c0);
     if (fq_eq(fq_sqr(s), a.c0)) {
       *out = {s, fp_zero<FqM>()};
       return true;
@@ -115,13 +139,8 @@ ZG_NOINL inline bool f2_sqrt(const Fq2& a, Fq2* out) {
     *out = {fp_zero<FqM>(), t};
     return fq_eq(fq_sqr(t), fq_neg(a.c0));
   }
-  const Fq n = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
-  const Fq g = fq_mul(fq_pow_pm3_4(n), n);
-  if (!fq_eq(fq_sqr(g), n)) return false;
-  const Fq d = fq_half(fq_add(a.c0, g));
-  const Fq e = fq_pow_pm3_4(d);
-  const Fq ed = fq_mul(e, d);
-  const Fq h = fq_half(fq_mul(a.c1, e));
+  const Fq ed = fq_mul(e0, d);
+  const Fq h = fq_half(fq_mul(a.c1, e0));
   Fq2 y;
   if (fq_eq(fq_sqr(ed), d))
     y = {ed, h};
