@@ -188,6 +188,8 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
     for (int q = S.bs(); q > 1; q >>= 1) h = jac_dbl_inl(h);  // BS = 2^k
     x = jac_add_full(x, h);
   }
+  // (the doubling chains run in lazy digits, zg_fqd.h: no split / repack / canonicalisation per
+  // product -- the window's 2^shift(w) chain is this kernel's critical path)
   __syncthreads();
   sh[s] = x;
   __syncthreads();
@@ -201,10 +203,11 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
     __syncthreads();
   }
   if (s == 0) {  // 2^shift(w) W_w: this window's part of sum_w 2^shift(w) W_w
-    G1J x = sh[0];
+    const G1J x = sh[0];
     const int w = g % S.w;
-    for (int q = 0; q < S.shift(w); q++) x = jac_dbl_inl(x);
-    m.wsum[g] = x;
+    G1D q = {fqd_from(x.x), fqd_from(x.y), fqd_from(x.z)};  // < 2p each: g1d_dbl's invariant holds
+    for (int k = 0; k < S.shift(w); k++) q = g1d_dbl(q);   // infinity (Z = 0) stays infinity
+    m.wsum[g] = g1d_to_jac(q);
   }
 }
 
