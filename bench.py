@@ -14,7 +14,7 @@ per-proof statuses. The host->HBM input copies are outside the timed region; h2d
 reports them. Inputs: real mainnet proofs from the reference's fixtures,
 re-randomized on the GPU (synthetic, all valid; verified OK after the timed region).
 Batch scalars r_i come from the OS RNG inside the timed region (production mode).
-Batches in flight (--inflight; default 4, or 6 on shards <= 16k proofs): each GPU keeps that many
+Batches in flight (--inflight; default 6): each GPU keeps that many
 consecutive batches on the device, one context (buffers + streams) each. The host reads the
 oldest batch's partial and statuses and relaunches its context at once; the batch's verdict
 (gather + final exponentiation, on a checker context) runs on a worker thread in batch order
@@ -264,7 +264,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--proofs", "--n", dest="n", type=int, default=65536, help="total proofs per step (all ranks)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight per GPU, one context each (0: 3 for shards > 16k proofs, else 6)")
+                    help="batches in flight per GPU, one context each (0: the default, 6)")
     ap.add_argument("--sync-verdict", action="store_true",
                     help="take each batch's verdict (gather + final exponentiation) before relaunching its context")
     ap.add_argument("--no-priority", action="store_true",
@@ -288,8 +288,10 @@ def main():
         # 4 -> 3.54, 5 -> 3.28, 6 -> 3.20, 8 -> 3.25, 10 -> 3.63 ms per batch; profiles/r02l_inflight_sweep.txt);
         # the slots share the device's fixed stream pool, so the round-1 limit of
         # 6 contexts per process no longer applies
-        # (65,536-proof shards, r02v: 2 -> 15.95, 3 -> 16.01, 4 -> 15.67, 5 -> 15.83 ms per batch)
-        args.inflight = 4 if args.n // world > 16384 else 6
+        # (65,536-proof shards, r02v: 2 -> 15.95, 3 -> 16.01, 4 -> 15.67, 5 -> 15.83 ms per batch; on the
+        # round-4 kernels, 5 alternating repeats: 4 -> 14.02, 6 -> 13.78, 8 -> 13.91 mean ms per batch,
+        # 6 the fastest in every repeat, profiles/r04y_inflight_64k.txt)
+        args.inflight = 6
     # two streams per context (main + side): give each its own hardware queue (set before the
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     # (RCCL's own streams want queues too: 8k shard over RCCL 5.58 ms/batch at 12 queues, 4.70 at 24)
