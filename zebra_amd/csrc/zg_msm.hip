@@ -1,6 +1,7 @@
 // zg_msm.hip -- translation unit of K4, the Pippenger MSM for sum r_i C_i per key and the root
 // Fr sums (zg_msm.h), plus the bisection-only per-proof C leaves.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "../../include/zg.h"
 #include "zg_msm.h"
@@ -287,6 +288,12 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
 hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate, hipEvent_t bucket0,
                            hipEvent_t bucket1, int k4) {
   m.s = msm_shape(b.npad);
+  // ZG_MSM_PARTS (tooling): lanes per bucket in the bucket phase, 1 / 2 / 4 / 8, kept only while a
+  // (key, window) group still fits one k_msm_group wave (nb / (64 / parts) <= ZG_MSM_SEG_MAX)
+  static const int parts_env = getenv("ZG_MSM_PARTS") ? atoi(getenv("ZG_MSM_PARTS")) : 0;
+  if ((parts_env == 1 || parts_env == 2 || parts_env == 4 || parts_env == 8) &&
+      m.s.nb / (64 / parts_env) <= ZG_MSM_SEG_MAX)
+    m.s.parts = parts_env;
   if (!k4) {
     hipError_t e;  // the bucket-phase events still bracket something (an empty phase): callers time them
     if (bucket0 && (e = hipEventRecord(bucket0, st)) != hipSuccess) return e;
