@@ -127,7 +127,7 @@ struct zg_ctx {
                           // product tree (measurement: the Miller kernels alone on the device)
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
-  Fq2* d_lines = nullptr;  // 68 x 3 x cap: the line hand-off R-chain -> f-chain (zg_batch.h line_at)
+  Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
   G1J* d_ctree = nullptr;
   Fr* d_stree = nullptr;
   MsmBufs msm = {};       // K4: Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)

@@ -19,12 +19,6 @@ namespace zg {
 
 __device__ __constant__ const int KIND_NINPUTS[ZG_NKINDS] = {7, 5, 9};
 
-// The line hand-off (R-chain -> f-chain, ZG_NCOEFF steps x 3 Fq2 per proof): coefficient j (A, B, C) of
-// step n of proof i at lines[(3 n + j) npad + i], so a coefficient's 64 proofs of a wave are contiguous
-// and its store writes whole cache lines (proof-major triples were written a coefficient at a time,
-// one third of each line per store: 1.67 GB written + 0.28 GB of fills against 1.28 GB, r04ag).
-ZG_INL size_t line_at(int n, int j, size_t npad, size_t proof) { return ((size_t)n * 3 + j) * npad + proof; }
-
 struct BatchBufs {
   const DevVK* vks;
   const uint8_t* proofs;   // n x 192

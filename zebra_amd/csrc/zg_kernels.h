@@ -72,8 +72,8 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
     for (int pass = 0; pass < 2; pass++) {
       if (pass == 1 && (i < 0 || !((ZG_XH >> i) & 1ull))) break;
       const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
-      Fq2* sink = proof < b.npad ? lines + line_at(n, 0, b.npad, proof) : nullptr;  // coefficient j at sink[j npad]
-      prog_run<true>(pid, atq, sink, act, b.npad);
+      Fq2* sink = proof < b.npad ? lines + ((size_t)n * b.npad + proof) * 3 : nullptr;
+      prog_run<true>(pid, atq, sink, act);
       Fq2 v;
       if (wave < 4) v = prog_output(PROG_INFO[pid].go + wave, atq);
       __syncthreads();
@@ -159,9 +159,10 @@ __device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines
   // the pair's two line triples are adjacent in [step][proof][3]
   auto load_lines = [&](int n) {
     wait_lines(n);
+    const Fq2* src = lines + ((size_t)n * b.npad + 2 * (size_t)pair) * 3;
     for (int j = wave - 6; j < 6; j += 2) {
       const bool act = j < 3 ? act0 : act1;
-      at.put(6 + j, act ? lines[line_at(n, j % 3, b.npad, 2 * (size_t)pair + j / 3)] : (j % 3 == 0 ? f2_one() : f2_zero()));
+      at.put(6 + j, act ? src[j] : (j % 3 == 0 ? f2_one() : f2_zero()));
     }
   };
   if (wave < 6)
@@ -229,8 +230,8 @@ __device__ __forceinline__ void fchain1_body(const BatchBufs& b, const Fq2* line
   };
   auto load_lines = [&](int n) {
     wait_lines(n);
-    const size_t pi = inb ? proof : 0;
-    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? lines[line_at(n, j, b.npad, pi)] : (j == 0 ? f2_one() : f2_zero()));
+    const Fq2* src = lines + ((size_t)n * b.npad + (inb ? proof : 0)) * 3;
+    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? src[j] : (j == 0 ? f2_one() : f2_zero()));
   };
   if (wave < 6)
     at.put(wave, wave == 0 ? f2_one() : f2_zero());
@@ -293,9 +294,10 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
 #pragma unroll
   for (int j = 0; j < 4; j++) actm |= (inb && proof_active(b, 4 * quad + j)) ? 1 << j : 0;
   auto load_lines = [&](int n) {
+    const Fq2* src = lines + ((size_t)n * b.npad + 4 * (size_t)quad) * 3;
     for (int j = (wave + 2) & 7; j < 12; j += 8) {
       const bool act = (actm >> (j / 3)) & 1;
-      at.put(6 + j, act ? lines[line_at(n, j % 3, b.npad, 4 * (size_t)quad + j / 3)] : (j % 3 == 0 ? f2_one() : f2_zero()));
+      at.put(6 + j, act ? src[j] : (j % 3 == 0 ? f2_one() : f2_zero()));
     }
   };
   if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
@@ -393,7 +395,8 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, cons
   const int proof = leaf ? node - b.npad : 0;
   const bool act = leaf && proof_active(b, proof);
   auto load_lines = [&](int n) {
-    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? lines[line_at(n, j, b.npad, proof)] : (j == 0 ? f2_one() : f2_zero()));
+    const Fq2* src = lines + ((size_t)n * b.npad + proof) * 3;
+    for (int j = wave - 6; j < 3; j += 2) at.put(6 + j, act ? src[j] : (j == 0 ? f2_one() : f2_zero()));
   };
   if (wave < 6)
     at.put(wave, wave == 0 ? f2_one() : f2_zero());

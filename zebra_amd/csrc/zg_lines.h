@@ -54,16 +54,16 @@ struct LinesHost {
 // pairing doubling_step (line_double of zg_pairing.h), the scaled line stored as soon as each
 // coefficient is known. tmp4 = 3 tmp0 is re-formed where used (two additions) instead of held.
 template <class St>
-ZG_INL void ls_double(St& st, const G1A* pa, Fq2* dst, bool act, size_t stride = 1) {
+ZG_INL void ls_double(St& st, const G1A* pa, Fq2* dst, bool act) {
   const Fq2 tmp1 = ls_sqr(st.get(1));
   const Fq2 zsq = ls_sqr(st.get(2));
   {
     const Fq2 nz = f2_sub(f2_sub(ls_sqr(f2_add(st.get(2), st.get(1))), tmp1), zsq);
-    dst[2 * stride] = act ? ls_mulfq(f2_dbl(ls_mul(nz, zsq)), pa->y) : f2_one();  // c0 py
+    dst[2] = act ? ls_mulfq(f2_dbl(ls_mul(nz, zsq)), pa->y) : f2_one();  // c0 py
     st.put(2, nz);
   }
   const Fq2 tmp0 = ls_sqr(st.get(0));
-  dst[stride] = act ? ls_mulfq(f2_neg(f2_dbl(ls_mul(f2_add(f2_dbl(tmp0), tmp0), zsq))), pa->x) : f2_one();  // c1 px
+  dst[1] = act ? ls_mulfq(f2_neg(f2_dbl(ls_mul(f2_add(f2_dbl(tmp0), tmp0), zsq))), pa->x) : f2_one();  // c1 px
   const Fq2 tmp5 = ls_sqr(f2_add(f2_dbl(tmp0), tmp0));
   dst[0] = act ? f2_sub(f2_sub(f2_sub(ls_sqr(f2_add(st.get(0), f2_add(f2_dbl(tmp0), tmp0))), tmp0), tmp5),
                         f2_dbl(f2_dbl(tmp1)))
@@ -78,7 +78,7 @@ ZG_INL void ls_double(St& st, const G1A* pa, Fq2* dst, bool act, size_t stride =
 // pairing addition_step (line_add of zg_pairing.h) with q affine (read from HBM where used), scaled
 // line. qy^2 is formed twice (one squaring per addition step, 5 per loop) instead of held.
 template <class St>
-ZG_INL void ls_add(St& st, const G2A* pq, const G1A* pa, Fq2* dst, bool act, size_t stride = 1) {
+ZG_INL void ls_add(St& st, const G2A* pq, const G1A* pa, Fq2* dst, bool act) {
   const Fq2 zsq = ls_sqr(st.get(2));
   const Fq2 t2 = f2_sub(ls_mul(zsq, pq->x), st.get(0));
   const Fq2 t6 = f2_sub(f2_sub(ls_mul(f2_sub(f2_sub(ls_sqr(f2_add(pq->y, st.get(2))), ls_sqr(pq->y)), zsq), zsq),
@@ -86,8 +86,8 @@ ZG_INL void ls_add(St& st, const G2A* pq, const G1A* pa, Fq2* dst, bool act, siz
                         st.get(1));
   const Fq2 t3 = ls_sqr(t2);
   st.put(2, f2_sub(f2_sub(ls_sqr(f2_add(st.get(2), t2)), zsq), t3));  // nz
-  dst[2 * stride] = act ? ls_mulfq(f2_dbl(st.get(2)), pa->y) : f2_one();       // c0 py
-  dst[stride] = act ? ls_mulfq(f2_dbl(f2_neg(t6)), pa->x) : f2_one();      // c1 px
+  dst[2] = act ? ls_mulfq(f2_dbl(st.get(2)), pa->y) : f2_one();       // c0 py
+  dst[1] = act ? ls_mulfq(f2_dbl(f2_neg(t6)), pa->x) : f2_one();      // c1 px
   {
     const Fq2 nz = st.get(2);
     const Fq2 t10 = f2_sub(f2_sub(ls_sqr(f2_add(pq->y, nz)), ls_sqr(pq->y)), ls_sqr(nz));

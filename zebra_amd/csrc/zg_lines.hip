@@ -38,12 +38,8 @@ __global__ void __launch_bounds__(64, WPE) k_batch_lines_lane(BatchBufs b, Fq2* 
   st.put(2, f2_one());
   int n = 0;
   for (int i = ZG_XH_TOP; i >= -1; i--) {
-    ls_double(st, pa, lines + line_at(n, 0, b.npad, proof), act, b.npad);
-    n++;
-    if (i >= 0 && ((ZG_XH >> i) & 1ull)) {
-      ls_add(st, pq, pa, lines + line_at(n, 0, b.npad, proof), act && chk, b.npad);
-      n++;
-    }
+    ls_double(st, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act);
+    if (i >= 0 && ((ZG_XH >> i) & 1ull)) ls_add(st, pq, pa, lines + ((size_t)(n++) * b.npad + proof) * 3, act && chk);
   }
   const G2J r = {st.get(0), st.get(1), st.get(2)};
   // r = [x] B (Jacobian). B in G2  <=>  psi(B) = [u] B = -[x] B  <=>  X = psi_x Z^2, Y = -psi_y Z^3,
