@@ -41,6 +41,36 @@ void zgt_g1_check_glv(const uint8_t* x, const uint8_t* y, uint64_t a, uint64_t b
   }
 }
 
+static void st_aff(const G1J& j, uint8_t* out) {
+  const G1A a = jac_to_aff(j);
+  memset(out, 0, 96);
+  if (!a.inf) {
+    st_fq(a.x, out);
+    st_fq(a.y, out + 48);
+  }
+}
+static G1J jac_scaled(const uint8_t* x, const uint8_t* y, const uint8_t* z) {
+  const Fq zz = ld_fq(z);
+  if (fq_is_zero(zz)) return jac_infinity<Fq>();
+  const Fq z2 = fq_sqr(zz);
+  return {fq_mul(ld_fq(x), z2), fq_mul(ld_fq(y), fq_mul(z2, zz)), zz};
+}
+static G1D g1d_of(const G1J& j) { return {fqd_from(j.x), fqd_from(j.y), fqd_from(j.z)}; }
+
+// K4's lazy-digit point sums (zg_fqd.h) against the word form (zg_curve.h): p = (x1, y1) and
+// q = (x2, y2) as Jacobian points scaled by z1 / z2 (zero: infinity). out_w / out_d: affine p + q
+// by jac_add_full / g1d_add_full; out_mw / out_md: p - (x2, y2) by jac_add_aff_inl / g1d_add_aff
+// with the negated y < 3p of the bucket phase (96 B each, zero bytes for infinity)
+void zgt_g1d_add(const uint8_t* x1, const uint8_t* y1, const uint8_t* z1, const uint8_t* x2, const uint8_t* y2,
+                 const uint8_t* z2, uint8_t* out_w, uint8_t* out_d, uint8_t* out_mw, uint8_t* out_md) {
+  const G1J p = jac_scaled(x1, y1, z1), q = jac_scaled(x2, y2, z2);
+  st_aff(jac_add_full(p, q), out_w);
+  st_aff(g1d_to_jac(g1d_add_full(g1d_of(p), g1d_of(q))), out_d);
+  const G1A qa = {ld_fq(x2), fq_neg(ld_fq(y2)), false};
+  st_aff(jac_add_aff_inl(p, qa), out_mw);
+  st_aff(g1d_to_jac(g1d_add_aff(g1d_of(p), fqd_from(ld_fq(x2)), fqd_neg2(fqd_from(ld_fq(y2))))), out_md);
+}
+
 // K4's signed-digit windows (zg_msm.h msm_shape / msm_digit) of the scalar lo + 2^64 hi for a
 // batch of npad padded proofs: digits[w], shifts[w], widths[w]; returns the window count, or -1
 // when the final carry is not zero; shape[] = c, w, nb, parts

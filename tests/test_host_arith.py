@@ -291,3 +291,29 @@ def test_g1_digit_arith_equals_word_form():
             assert res[2] == 1 or not ing1   # the two-column GLV (decode's) agrees on G1 points
             if ing1 and a == 0 and b == 0:   # k = 1: r A = A
                 assert ow.raw == fq_b(x) + fq_b(y)
+
+
+def test_g1_digit_point_sums_equal_word_form():
+    """K4's lazy-digit sums (zg_fqd.h g1d_add_full: merges, scans, trees; g1d_add_aff with the
+    bucket phase's negated y < 3p) against the word form on random Jacobian scalings: generic sums,
+    P + P (doubling), P + (-P) (infinity), infinity on either side, points outside G1"""
+    import ctypes
+    L = hostlib.lib()
+    L.zgt_g1d_add.argtypes = [ctypes.c_char_p] * 6 + [ctypes.c_char_p] * 4
+    rng = random.Random(11)
+    pts = [p for p, _ in _g1_points(rng, 4)]
+    z = lambda: fq_b(rng.randrange(1, P))
+    zero = fq_b(0)
+    cases = []
+    for a in pts:
+        for b in pts:
+            cases.append((a, z(), b, z()))
+        cases.append((a, z(), a, z()))                      # doubling
+        cases.append((a, z(), (a[0], P - a[1]), z()))      # infinity
+        cases.append((a, zero, a, z()))                     # inf + q
+        cases.append((a, z(), a, zero))                     # p + inf
+    for (x1, y1), z1, (x2, y2), z2 in cases:
+        ow, od, mw, md = (ctypes.create_string_buffer(96) for _ in range(4))
+        L.zgt_g1d_add(fq_b(x1), fq_b(y1), z1, fq_b(x2), fq_b(y2), z2, ow, od, mw, md)
+        assert ow.raw == od.raw
+        assert mw.raw == md.raw

@@ -308,6 +308,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->msm.start, ZG_MSM_NCOUNT_MAX + 1));
   A(dalloc(&ctx->msm.cursor, ZG_MSM_NCOUNT_MAX));
   A(dalloc(&ctx->msm.entries, 2 * (size_t)cap * ZG_MSM_WMAX));
+  A(dalloc(&ctx->msm.cd, (size_t)cap * ZG_MSM_CD));
   A(dalloc(&ctx->msm.seg, (size_t)ZG_MSM_GROUPS_MAX * ZG_MSM_SEG_MAX * 2));
   A(dalloc(&ctx->msm.wsum, ZG_MSM_GROUPS_MAX));
   A(dalloc(&ctx->msm.frpart, ((size_t)cap / ZG_FR_CHUNK + 1) * ZG_NKINDS * ZG_MAX_IC));
@@ -346,7 +347,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
-                  ctx->msm.entries, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
+                  ctx->msm.entries, ctx->msm.cd, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
                   ctx->bn_arena, ctx->d_dbg};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -683,8 +684,8 @@ static int launch_node_msm_pairs(zg_ctx* ctx, const BatchBufs& b, const NodeBufs
 
 namespace zg {
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv);  // zg_decode.hip
-hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate,
-                           hipEvent_t bucket0 = nullptr, hipEvent_t bucket1 = nullptr, int k4 = 1);          // zg_msm.hip
+hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate, hipEvent_t bucket0,
+                           hipEvent_t bucket1, int k4, bool alone);                                       // zg_msm.hip
 hipError_t launch_c_leaves(hipStream_t st, const BatchBufs& b);                                // zg_msm.hip
 hipError_t launch_lines_lane(unsigned groups, hipStream_t st, const BatchBufs& b, Fq2* lines, int wpe);  // zg_lines.hip
 // the staged-program kernels of zg_kernels.h, one translation unit each (zg_prog_*.hip)
@@ -743,7 +744,7 @@ static int run_pipeline(zg_ctx* ctx) {
   // side stream: K4 + the root's VK-side work (or, serial_side, on the main stream after the tree)
   auto side_work = [&](hipStream_t st) -> int {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
-    HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9], k4));
+    HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9], k4, alone));
     if (!k4) HIPCHK(launch_c_tree(ctx, b, st, nullptr));
     HIPCHK(hipEventRecord(ctx->ev[10], st));
     int r = launch_node_msm_pairs(ctx, b, nb, st);
@@ -821,7 +822,7 @@ static int run_pipeline(zg_ctx* ctx) {
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream K4 + root pairs complete
   }
   // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
-  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail, nullptr, nullptr, k4));
+  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail, nullptr, nullptr, k4, alone));
   if (!k4) HIPCHK(launch_c_tree(ctx, b, ctx->stream, b.bfail));
   rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
   if (rc) return rc;

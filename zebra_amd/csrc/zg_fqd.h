@@ -266,6 +266,36 @@ ZG_INL G1D g1d_add_aff(const G1D& p, const FqD& qx, const FqD& qy) {
   return {X3, Y3, Z3};
 }
 
+// add-2007-bl with complete case handling: p + q, both in the invariant (either may be infinity).
+// Out: X < 9p, Y < 7p, Z < 4p (or g1d_dbl's, or p / q itself). 16 products.
+ZG_INL G1D g1d_add_full(const G1D& p, const G1D& q) {
+  if (g1d_is_inf(p)) return q;
+  if (g1d_is_inf(q)) return p;
+  const FqD Z1Z1 = fqd_sqr(p.z);                           // (Z1 < 4)^2: < 2
+  const FqD Z2Z2 = fqd_sqr(q.z);                           // < 2
+  const FqD U1 = fqd_mul(p.x, Z2Z2);                       // 35 x 2: < 2
+  const FqD U2 = fqd_mul(q.x, Z1Z1);                       // < 2
+  const FqD S1 = fqd_mul(fqd_mul(p.y, q.z), Z2Z2);         // (19 x 4 -> < 2) x 2: < 2
+  const FqD S2 = fqd_mul(fqd_mul(q.y, p.z), Z1Z1);         // < 2
+  const FqD H = fqd_sub<3, 1, 1>(U2, U1);                  // U2 - U1 + 3p: < 5 (U1 < 2)
+  const FqD rr = fqd_sub<5, 2, 2>(S2, S1);                 // 2 S2 - 2 S1 + 5p: < 9 (2 S1 < 4)
+  const FqD HH = fqd_sqr(H);                               // < 2
+  const FqD RR = fqd_sqr(rr);                              // < 2
+  // H == 0 mod p <=> H^2 == 0 (and rr likewise): P == +-Q
+  if (fqd_is_zero2(HH)) {
+    if (fqd_is_zero2(RR)) return g1d_dbl(p);
+    return g1d_infinity();
+  }
+  const FqD I = fqd_smul<4>(HH);                           // (2H)^2: < 8
+  const FqD J = fqd_mul(H, I);                             // 5 x 8: < 2
+  const FqD V = fqd_mul(U1, I);                            // < 2
+  const FqD X3 = fqd_sub2<7>(RR, J, fqd_smul<2>(V));       // rr^2 - J - 2V + 7p: < 9 (J + 2V < 6)
+  const FqD Y3a = fqd_mul(rr, fqd_sub<10, 1, 1>(V, X3));   // (V - X3 + 10p < 12) x (rr < 9): < 2
+  const FqD Y3 = fqd_sub<5, 1, 2>(Y3a, fqd_mul(S1, J));    // - 2 S1 J + 5p: < 7 (2 S1 J < 4)
+  const FqD Z3 = fqd_smul<2>(fqd_mul(fqd_mul(p.z, q.z), H));  // 2 Z1 Z2 H: (16 -> < 2) x 5 -> < 2, x 2: < 4
+  return {X3, Y3, Z3};
+}
+
 // -x for x < 2p: 3p - x < 3p
 ZG_INL FqD fqd_neg2(const FqD& x) { return fqd_sub<3, 0, 1>(fqd_zero(), x); }
 

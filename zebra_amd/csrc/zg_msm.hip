@@ -18,11 +18,25 @@ ZG_INL void msm_scalar(const BatchBufs& b, int i, int j, uint64_t* lo, uint32_t*
 
 ZG_INL bool msm_live(const BatchBufs& b, int i) { return i < b.n && b.status[i] == ST_PENDING; }
 
+// lane (proof i, point j): the bucket sizes; lanes (i, 0) and (i, 1) also write C_i's digit
+// operands once for the bucket phase: (x, y) and beta x respectively (zg_fqd.h FqD, < 2p each)
 __global__ void __launch_bounds__(64) k_msm_count(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = t >> 1, j = t & 1;
   if (i >= b.npad || !msm_live(b, i)) return;
+  {
+    const G1A c = b.ptAC[(size_t)b.npad + i];
+    uint32_t* row = m.cd + (size_t)i * ZG_MSM_CD;
+    const FqD u = j ? fqd_from(fq_mul(c.x, fq_const(G1_BETA))) : fqd_from(c.x);
+#pragma unroll
+    for (int q = 0; q < 14; q++) row[16 * j + q] = u.d[q];
+    if (!j) {
+      const FqD y = fqd_from(c.y);
+#pragma unroll
+      for (int q = 0; q < 14; q++) row[32 + q] = y.d[q];
+    }
+  }
   const MsmShape S = m.s;
   const int kind = b.kinds[i];
   uint64_t lo;
@@ -86,129 +100,161 @@ __global__ void __launch_bounds__(64) k_msm_scatter(BatchBufs b, MsmBufs m, cons
   }
 }
 
+// 14 digits of an FqD operand row (16 words, 4 x uint4; the last two words are padding)
+ZG_INL FqD msm_ld_digits(const uint32_t* row) {
+  const uint4* v = (const uint4*)row;
+  const uint4 a = v[0], c = v[1], d = v[2], e = v[3];
+  return FqD{{a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w, e.x, e.y}};
+}
+
+// whether (key, window) group g holds any entry (a key absent from the batch: none)
+ZG_INL bool msm_group_live(const MsmBufs& m, int g) { return m.start[(g + 1) * m.s.nb] > m.start[g * m.s.nb]; }
+
 // The bucket phase with the first reduction level (see zg_msm.h). Wave gw of the grid holds
-// buckets [gw BS, (gw + 1) BS) (BS = 64 / P, inside one (key, window) group), lane = (bucket j,
-// part); the segment's outputs are T = sum_j (j + 1) S_j and U = sum_j S_j.
+// segment gw: buckets [gw BS, (gw + 1) BS) (BS = 64 / P, inside one (key, window) group), lane =
+// (bucket j, part); the segment's outputs are T = sum_j (j + 1) S_j and U = sum_j S_j. LDS: the
+// waves' staged entries, then (the same bytes) the block's lane points for the reductions.
 __global__ void __launch_bounds__(ZG_MSM_BT) k_msm_bucket(BatchBufs b, MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  __shared__ G1J sh[ZG_MSM_BT];
+  constexpr int NW = ZG_MSM_BT / 64;
+  constexpr int WORDS = NW * ZG_MSM_STAGE > ZG_MSM_BT * (int)(sizeof(G1D) / 4) ? NW * ZG_MSM_STAGE
+                                                                               : ZG_MSM_BT * (int)(sizeof(G1D) / 4);
+  __shared__ uint32_t lds[WORDS];
+  G1D* sh = (G1D*)lds;
   const MsmShape S = m.s;
-  const int lane = threadIdx.x & 63, w0 = threadIdx.x & ~63;
-  const int gw = blockIdx.x * (ZG_MSM_BT / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, w0 = threadIdx.x & ~63;
+  const int gw = blockIdx.x * NW + wv;
   const int P = S.parts, BS = S.bs();
-  const bool live = gw * BS < S.ncount();  // whole waves are live or not
+  // whole waves are live or not: past the grid's buckets, or a group without entries
+  const bool live = gw * BS < S.ncount() && msm_group_live(m, gw / S.nseg());
   const int j = lane / P, part = lane % P;
-  G1J acc = jac_infinity<Fq>();
+  // stage the segment's sorted entries in LDS (coalesced); a segment past the stage reads in place
+  const int slo = live ? m.start[gw * BS] : 0, shi = live ? m.start[(gw + 1) * BS] : 0;
+  const bool staged = shi - slo <= ZG_MSM_STAGE;
+  uint32_t* st = lds + wv * ZG_MSM_STAGE;
+  if (live && staged)
+    for (int e = lane; e < shi - slo; e += 64) st[e] = m.entries[slo + e];
+  __syncthreads();
+  G1D acc = g1d_infinity();
   if (live) {
     const int bucket = gw * BS + j;
     const int lo = m.start[bucket], len = m.start[bucket + 1] - lo;
     const int beg = lo + len * part / P, end = lo + len * (part + 1) / P;
-    const Fq beta = fq_const(G1_BETA);
     // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
     // status between count and scatter -- then bfail > 0 and the gated recompute redoes it; it
-    // must still stay inside the buffers). The next entry's point is gathered while the current
-    // one is added (software pipelining: its L2 / HBM latency hides behind the addition).
-    auto gather = [&](int e, uint32_t* ent, G1A* c) {
-      *ent = m.entries[e];
-      const uint32_t pi = *ent >> 2;
-      *c = b.ptAC[(size_t)b.npad + (pi < (uint32_t)b.npad ? pi : 0)];
+    // must still stay inside the buffers). The next entry's operands are gathered while the
+    // current one is added: their L2 / HBM latency hides behind the addition.
+    auto entry = [&](int e) { return staged ? st[e - slo] : m.entries[e]; };
+    auto gather = [&](uint32_t ent, FqD* x, FqD* y) {
+      const uint32_t pi = ent >> 2;
+      const uint32_t* row = m.cd + (size_t)(pi < (uint32_t)b.npad ? pi : 0) * ZG_MSM_CD;
+      *x = msm_ld_digits(row + ((ent & 2u) ? 16 : 0));
+      *y = msm_ld_digits(row + 32);
     };
     uint32_t ent_n = 0;
-    G1A c_n;
-    if (beg < end) gather(beg, &ent_n, &c_n);
+    FqD x_n, y_n;
+    if (beg < end) {
+      ent_n = entry(beg);
+      gather(ent_n, &x_n, &y_n);
+    }
     for (int e = beg; e < end; e++) {
       const uint32_t ent = ent_n;
-      const G1A c = c_n;
-      if (e + 1 < end) gather(e + 1, &ent_n, &c_n);
+      const FqD x = x_n, y = y_n;
+      if (e + 1 < end) {
+        ent_n = entry(e + 1);
+        gather(ent_n, &x_n, &y_n);
+      }
       if ((ent >> 2) >= (uint32_t)b.npad) continue;
-      const Fq x = (ent & 2u) ? fq_mul(c.x, beta) : c.x;
-      const Fq y = (ent & 1u) ? fq_neg(c.y) : c.y;
-      acc = jac_add_aff_inl(acc, G1A{x, y, false});
+      acc = g1d_add_aff(acc, x, (ent & 1u) ? fqd_neg2(y) : y);  // x < 2p, y < 3p
     }
   }
+  __syncthreads();  // the stage is read: its bytes become the lane points
   // merge the P parts of each bucket: S_j lands in lane j P
   sh[threadIdx.x] = acc;
   __syncthreads();
   for (int d = 1; d < P; d <<= 1) {
-    G1J v = sh[threadIdx.x];
-    if (part % (2 * d) == 0) v = jac_add_full(v, sh[threadIdx.x + d]);
+    G1D v = sh[threadIdx.x];
+    if (part % (2 * d) == 0) v = g1d_add_full(v, sh[threadIdx.x + d]);
     __syncthreads();
     sh[threadIdx.x] = v;
     __syncthreads();
   }
   // compact: lane j < BS holds S_j
-  G1J v = lane < BS ? sh[w0 + lane * P] : jac_infinity<Fq>();
-  __syncthreads();
-  sh[threadIdx.x] = v;
-  __syncthreads();
+  if (P > 1) {
+    G1D v = lane < BS ? sh[w0 + lane * P] : g1d_infinity();
+    __syncthreads();
+    sh[threadIdx.x] = v;
+    __syncthreads();
+  }
   // suffix sums H_j = sum_{j' >= j} S_j' (inclusive Hillis-Steele, BS lanes)
   for (int d = 1; d < BS; d <<= 1) {
-    G1J u = sh[threadIdx.x];
-    if (lane + d < BS) u = jac_add_full(u, sh[threadIdx.x + d]);
+    G1D u = sh[threadIdx.x];
+    if (lane + d < BS) u = g1d_add_full(u, sh[threadIdx.x + d]);
     __syncthreads();
     sh[threadIdx.x] = u;
     __syncthreads();
   }
-  const G1J U = sh[w0];  // H_0
+  // U = H_0, written at once (held across the tree it would live in the private segment)
+  const bool out = gw * BS < S.ncount() && lane == 0;  // (a group without entries writes infinity)
+  G1D* seg = m.seg + ((size_t)(gw / S.nseg()) * ZG_MSM_SEG_MAX + gw % S.nseg()) * 2;
+  if (out) seg[1] = sh[w0];
   // T = sum_j H_j: tree over the BS suffix sums
   for (int d = BS / 2; d >= 1; d >>= 1) {
-    G1J u = sh[threadIdx.x];
-    if (lane < d) u = jac_add_full(u, sh[threadIdx.x + d]);
+    G1D u = sh[threadIdx.x];
+    if (lane < d) u = g1d_add_full(u, sh[threadIdx.x + d]);
     __syncthreads();
     sh[threadIdx.x] = u;
     __syncthreads();
   }
-  if (live && lane == 0) {
-    const int g = gw / S.nseg(), s = gw % S.nseg();
-    m.seg[((size_t)g * ZG_MSM_SEG_MAX + s) * 2 + 0] = sh[w0];
-    m.seg[((size_t)g * ZG_MSM_SEG_MAX + s) * 2 + 1] = U;
-  }
+  if (out) seg[0] = sh[w0];
 }
 
 // one wave per (key, window) group: sum_b (b + 1) S_b = sum_s (T_s + BS s U_s), with
-// sum_s s U_s = sum_{s >= 1} H_s, H_s = sum_{s' >= s} U_s' (lane s = segment s)
+// sum_s s U_s = sum_{s >= 1} H_s, H_s = sum_{s' >= s} U_s' (lane s = segment s). Lazy digits
+// throughout (zg_fqd.h): the window's 2^shift(w) doubling chain is this kernel's critical path.
 __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
   if (gate && *gate == 0) return;
-  __shared__ G1J sh[64];
+  __shared__ G1D sh[64];
   const MsmShape S = m.s;
   const int g = blockIdx.x, s = threadIdx.x, ns = S.nseg();
-  const G1J* sg = m.seg + (size_t)g * ZG_MSM_SEG_MAX * 2;
-  const G1J T = s < ns ? sg[2 * s] : jac_infinity<Fq>();
-  sh[s] = s < ns ? sg[2 * s + 1] : jac_infinity<Fq>();
+  if (!msm_group_live(m, g)) {  // a key absent from the batch (wave-uniform)
+    if (s == 0) m.wsum[g] = g1d_infinity();
+    return;
+  }
+  const G1D* sg = m.seg + (size_t)g * ZG_MSM_SEG_MAX * 2;
+  const G1D T = s < ns ? sg[2 * s] : g1d_infinity();
+  sh[s] = s < ns ? sg[2 * s + 1] : g1d_infinity();
   __syncthreads();
   for (int d = 1; d < ns; d <<= 1) {
-    G1J u = sh[s];
-    if (s + d < ns) u = jac_add_full(u, sh[s + d]);
+    G1D u = sh[s];
+    if (s + d < ns) u = g1d_add_full(u, sh[s + d]);
     __syncthreads();
     sh[s] = u;
     __syncthreads();
   }
-  G1J x = T;
+  G1D x = T;
   if (s >= 1 && s < ns) {
-    G1J h = sh[s];
-    for (int q = S.bs(); q > 1; q >>= 1) h = jac_dbl_inl(h);  // BS = 2^k
-    x = jac_add_full(x, h);
+    G1D h = sh[s];
+    for (int q = S.bs(); q > 1; q >>= 1) h = g1d_dbl(h);  // BS = 2^k
+    x = g1d_add_full(x, h);
   }
-  // (the doubling chains run in lazy digits, zg_fqd.h: no split / repack / canonicalisation per
-  // product -- the window's 2^shift(w) chain is this kernel's critical path)
   __syncthreads();
   sh[s] = x;
   __syncthreads();
   int top = 1;
   while (top < ns) top <<= 1;
   for (int d = top / 2; d >= 1; d >>= 1) {  // the lanes past ns hold infinity
-    G1J u = sh[s];
-    if (s < d) u = jac_add_full(u, sh[s + d]);
+    G1D u = sh[s];
+    if (s < d) u = g1d_add_full(u, sh[s + d]);
     __syncthreads();
     sh[s] = u;
     __syncthreads();
   }
   if (s == 0) {  // 2^shift(w) W_w: this window's part of sum_w 2^shift(w) W_w
-    const G1J x = sh[0];
+    G1D q = sh[0];
     const int w = g % S.w;
-    G1D q = {fqd_from(x.x), fqd_from(x.y), fqd_from(x.z)};  // < 2p each: g1d_dbl's invariant holds
-    for (int k = 0; k < S.shift(w); k++) q = g1d_dbl(q);   // infinity (Z = 0) stays infinity
-    m.wsum[g] = g1d_to_jac(q);
+    for (int k = 0; k < S.shift(w); k++) q = g1d_dbl(q);  // infinity (Z = 0) stays infinity
+    m.wsum[g] = q;
   }
 }
 
@@ -218,9 +264,9 @@ __global__ void __launch_bounds__(64) k_msm_final(BatchBufs b, MsmBufs m, const 
   const int kind = threadIdx.x;
   if (kind >= ZG_NKINDS) return;
   const MsmShape S = m.s;
-  G1J acc = m.wsum[kind * S.w];
-  for (int w = 1; w < S.w; w++) acc = jac_add_full(acc, m.wsum[kind * S.w + w]);
-  b.ctree[1 * ZG_NKINDS + kind] = acc;
+  G1D acc = m.wsum[kind * S.w];
+  for (int w = 1; w < S.w; w++) acc = g1d_add_full(acc, m.wsum[kind * S.w + w]);
+  b.ctree[1 * ZG_NKINDS + kind] = g1d_to_jac(acc);
 }
 
 // root Fr sums from the stree leaves (decode_finish: r_i, r_i x_ij in the proof's kind, zero
@@ -285,15 +331,10 @@ __global__ void __launch_bounds__(64, 2) k_c_leaves(BatchBufs b) {
 // the batch root's C sums (ctree node 1) and Fr sums (stree node 1) from the decoded batch;
 // gate: null = always, else only if *gate != 0 (the recompute after a deferred B failure)
 // k4 = 0 (small shards): only the root Fr sums; the C sums are the tree levels of the GLV leaves
+// alone: no other batch on the device (the bucket phase's lanes per bucket: zg_msm.h)
 hipError_t launch_msm_root(hipStream_t st, const BatchBufs& b, MsmBufs m, const int* gate, hipEvent_t bucket0,
-                           hipEvent_t bucket1, int k4) {
-  m.s = msm_shape(b.npad);
-  // ZG_MSM_PARTS (tooling): lanes per bucket in the bucket phase, 1 / 2 / 4 / 8, kept only while a
-  // (key, window) group still fits one k_msm_group wave (nb / (64 / parts) <= ZG_MSM_SEG_MAX)
-  static const int parts_env = getenv("ZG_MSM_PARTS") ? atoi(getenv("ZG_MSM_PARTS")) : 0;
-  if ((parts_env == 1 || parts_env == 2 || parts_env == 4 || parts_env == 8) &&
-      m.s.nb / (64 / parts_env) <= ZG_MSM_SEG_MAX)
-    m.s.parts = parts_env;
+                           hipEvent_t bucket1, int k4, bool alone) {
+  m.s = msm_shape(b.npad, alone);
   if (!k4) {
     hipError_t e;  // the bucket-phase events still bracket something (an empty phase): callers time them
     if (bucket0 && (e = hipEventRecord(bucket0, st)) != hipSuccess) return e;
