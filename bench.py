@@ -296,6 +296,8 @@ def main():
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     # (RCCL's own streams want queues too: 8k shard over RCCL 5.58 ms/batch at 12 queues, 4.70 at 24)
     hwq = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 24))
+    if os.environ.get("ZG_BENCH_HWQ"):   # (tooling: an exact queue count for the sweeps in tools/gpu_r05.sh)
+        hwq = min(32, int(os.environ["ZG_BENCH_HWQ"]))
     os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch
     import torch.distributed as dist
@@ -345,8 +347,12 @@ def main():
     d_inputs = torch.frombuffer(bytearray(inputs), dtype=torch.uint8).to(dev)
     timings = []
 
+    ltime = []   # host seconds per batch in zg_batch_begin_device (the pipeline's launches)
+
     def launch(c):
+        t0 = time.perf_counter()
         c.batch_begin_device(shard, d_proofs.data_ptr(), d_kinds.data_ptr(), d_inputs.data_ptr())
+        ltime.append(time.perf_counter() - t0)
 
     host = []   # per batch: host seconds waiting for the partial, in the exchange + check, in finish
 
@@ -390,7 +396,7 @@ def main():
     def run(k):
         if args.sync_verdict:
             return run_pipelined(ctxs, k, launch, complete)
-        return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo)
+        return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=lambda c: c.batch_ready())
 
     def barrier():
         if use_dist:
@@ -401,6 +407,7 @@ def main():
     timings.clear()
     host.clear()
     vtime.clear()
+    ltime.clear()
     barrier()
     t0 = time.perf_counter()
     results = run(args.steps)
@@ -509,8 +516,8 @@ def main():
         "job_roofline_frac": value * W_TOTAL * MACS_PER_FQMUL / peak,
         "phase_ms": dict(zip(names, avg)),
         "h2d_ms_per_batch": h2d,
-        "host_ms_per_batch": {"wait_partial": host_ms[0], "exchange_and_final_exp": host_ms[1],
-                              "statuses": host_ms[2],
+        "host_ms_per_batch": {"launch": 1e3 * sum(ltime) / max(1, len(ltime)), "wait_partial": host_ms[0],
+                              "exchange_and_final_exp": host_ms[1], "statuses": host_ms[2],
                               "verdict": "sync" if args.sync_verdict else "deferred (worker thread, checker context)"},
     }
     if rank == 0 and world == 1 and not args.no_configs:

@@ -142,6 +142,11 @@ int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* 
 int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,
                           const void* d_inputs, const void* d_n_inputs, const void* d_r);
 int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
+/* zg_batch_ready: 1 when the batch begun on ctx has finished its device work (zg_batch_partial and
+ * a true-verdict zg_batch_finish then return without waiting), 0 while it runs, < 0 on error. It
+ * never blocks: a host loop keeping several batches in flight harvests whichever finishes first
+ * (batches in flight finish out of order). */
+int zg_batch_ready(zg_ctx* ctx);
 int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
 int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);
 /* zg_set_priority: recreate the context's two streams at the device's highest (high != 0) or
@@ -294,8 +299,9 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
  * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
  * (k_batch_fchain4; shards of 8,192 or more padded proofs -- ZG_QUAD_MIN -- or as ZG_FCHAIN_QUADS
- * forces), [8] zg_pghr13_verify calls with proofs, [9] those whose one batch check failed (the
- * call then ran the per-proof check for the exact statuses), [10] batches whose sums r_i C_i came
+ * forces), [8] zg_pghr13_verify calls with proofs (once per call, however many 65,536-proof chunks it
+ * took), [9] those in which a chunk's batch check failed (that chunk then ran the per-proof check
+ * for the exact statuses), [10] batches whose sums r_i C_i came
  * from the GLV products in decode and the C-sum tree (shards below 16,384 padded proofs -- ZG_K4_MIN
  * -- instead of K4's Pippenger buckets; [6] is 0 for them). Writes min(n, 11) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);

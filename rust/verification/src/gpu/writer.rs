@@ -180,7 +180,7 @@ impl<'a, S: BlockStore<B>, B: ImportBlock, V: Backend> DeferredBlocksWriter<'a, 
             }
         }
         // verify BEFORE the window is taken: on a backend failure the window and the pending
-        // set stay as they were, so `retry_on` (or a later flush) can still verify them
+        // set stay as they were, so `flush_with` (or a later flush) can still verify them
         let res: Option<(usize, TxError)> = if flat.is_empty() {
             None
         } else {
@@ -208,4 +208,130 @@ impl<'a, S: BlockStore<B>, B: ImportBlock, V: Backend> DeferredBlocksWriter<'a, 
 
 fn clone_tx(t: &Tx) -> Tx {
     t.clone()
+}
+
+#[cfg(test)]
+mod tests {
+    //! The Python mirror's test_backend_failure_keeps_the_window (tests/test_blocks_writer.py):
+    //! a backend that fails twice leaves the window held and the storage untouched; flush_with on
+    //! another backend then gives the sequential writer's storage and first error.
+    use super::super::collect::JoinSplit;
+    use super::super::ffi::{ZG_STATUS_OK, ZG_STATUS_VERIFY_FAILED};
+    use super::super::Item;
+    use super::*;
+    use std::cell::Cell;
+
+    #[derive(Clone)]
+    struct TBlock {
+        h: [u8; 32],
+        p: [u8; 32],
+        txs: Vec<Tx>,
+    }
+    impl ImportBlock for TBlock {
+        fn hash(&self) -> [u8; 32] {
+            self.h
+        }
+        fn parent(&self) -> [u8; 32] {
+            self.p
+        }
+        fn precheck(&self, _known: &dyn Fn(&[u8; 32]) -> bool) -> Result<(), String> {
+            Ok(())
+        }
+        fn txs(&self) -> &[Tx] {
+            &self.txs
+        }
+    }
+
+    #[derive(Default)]
+    struct TStore {
+        order: Vec<[u8; 32]>,
+        set: HashSet<[u8; 32]>,
+    }
+    impl BlockStore<TBlock> for TStore {
+        fn contains(&self, h: &[u8; 32]) -> bool {
+            self.set.contains(h)
+        }
+        fn insert(&mut self, b: TBlock) -> Result<(), String> {
+            self.set.insert(b.h);
+            self.order.push(b.h);
+            Ok(())
+        }
+    }
+
+    /// statuses from the proof's first byte (0xEE: VERIFY_FAILED); the first `fails` calls fail
+    struct Flaky {
+        fails: Cell<u32>,
+    }
+    impl Backend for Flaky {
+        fn verify(&self, items: &[Item]) -> Result<Vec<u8>, GpuError> {
+            if self.fails.get() > 0 {
+                self.fails.set(self.fails.get() - 1);
+                return Err(GpuError { code: -1, message: "device lost".to_string() });
+            }
+            Ok(items.iter().map(|it| if it.proof[0] == 0xEE { ZG_STATUS_VERIFY_FAILED } else { ZG_STATUS_OK }).collect())
+        }
+        fn pghr13_verify(&self, items: &[([u8; 296], Vec<[u8; 32]>)]) -> Result<Vec<u8>, GpuError> {
+            Ok(vec![ZG_STATUS_OK; items.len()])
+        }
+        fn redjubjub_verify(&self, items: &[([u8; 32], [u8; 64], [u8; 64], u8)]) -> Result<Vec<bool>, GpuError> {
+            Ok(vec![true; items.len()])
+        }
+        fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError> {
+            Ok(vec![(0, [0u8; 32]); txs.len()])
+        }
+    }
+
+    /// block i + 1 on parent i: one transaction with one Groth16 JoinSplit
+    fn block(i: u8, bad: bool) -> TBlock {
+        let mut proof = [0u8; 192];
+        proof[0] = if bad { 0xEE } else { 0x01 };
+        let js = JoinSplit {
+            anchor: [i; 32],
+            random_seed: [1; 32],
+            nullifiers: [[2; 32], [3; 32]],
+            macs: [[4; 32], [5; 32]],
+            commitments: [[6; 32], [7; 32]],
+            vpub_old: 0,
+            vpub_new: 0,
+            groth_proof: Some(proof),
+            pghr_proof: None,
+            pghr_ok: None,
+            tree_error: None,
+        };
+        let tx = Tx { js_pubkey: Some([9; 32]), js_sig_ok: true, joinsplits: vec![js], ..Default::default() };
+        TBlock { h: [i + 1; 32], p: [i; 32], txs: vec![tx] }
+    }
+
+    #[test]
+    fn backend_failure_keeps_the_window() {
+        // genesis [0; 32] stored; blocks 1..=6 with block 4's proof failing
+        let blocks: Vec<TBlock> = (0u8..6).map(|i| block(i, i == 3)).collect();
+        let mut st = TStore::default();
+        st.set.insert([0u8; 32]);
+        let gpu = Flaky { fails: Cell::new(2) };
+        let cpu = Flaky { fails: Cell::new(0) };
+        let mut w = DeferredBlocksWriter::new(st, &gpu, 1 << 20);
+        for b in blocks.iter().cloned() {
+            w.append_block(b).unwrap();
+        }
+        for _ in 0..2 {
+            match w.flush() {
+                Err(WriterError::Backend(e)) => assert_eq!(e.message, "device lost"),
+                other => panic!("expected a backend failure, got {:?}", other.err()),
+            }
+            assert!(w.storage().order.is_empty());
+            assert_eq!(w.window.len(), 6);
+            assert!(blocks.iter().all(|b| w.known(&b.h)));
+        }
+        // the sequential writer's outcome: blocks 1..=3 inserted, block 4's JoinSplit reported
+        match w.flush_with(&cpu) {
+            Err(WriterError::Verification(e)) => {
+                assert_eq!(e, format!("transaction 0: {:?}", TxError::InvalidJoinSplit(0)))
+            }
+            other => panic!("expected block 4's verification error, got {:?}", other.err()),
+        }
+        let want: Vec<[u8; 32]> = (1u8..4).map(|i| [i; 32]).collect();
+        assert_eq!(w.storage().order, want);
+        assert!(w.window.is_empty());
+    }
 }

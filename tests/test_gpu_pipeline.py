@@ -11,7 +11,8 @@ from tests.test_gpu_parity import corrupted_4096
 pytestmark = pytest.mark.gpu
 
 
-def test_deferred_verdicts_exact_statuses():
+@pytest.mark.parametrize("poll", [False, True], ids=["in-order", "first-ready"])
+def test_deferred_verdicts_exact_statuses(poll):
     from zebra_amd import Context, pack_inputs
     from zebra_amd.dist import run_pipelined_deferred
     n = 4096
@@ -52,7 +53,8 @@ def test_deferred_verdicts_exact_statuses():
             ok = c.gt_check([c.batch_partial()])
             return c.batch_finish(ok, n)
 
-        res = run_pipelined_deferred(cs, 5, launch, harvest, verdict, redo)
+        res = run_pipelined_deferred(cs, 5, launch, harvest, verdict, redo,
+                                     ready=(lambda c: c.batch_ready()) if poll else None)
         assert [ok for ok, _ in res] == [True, True, False, True, True]
         for b, (_, sts) in enumerate(res):
             assert sts == batches[b][3], b

@@ -1,0 +1,64 @@
+"""CPU tier: the host schedule of batches in flight (zebra_amd.dist.run_pipelined_deferred) with
+contexts that finish OUT of launch order, as batches sharing a device do. The loop must harvest
+whichever batch is ready first, relaunch its context at once, still run the verdicts (the
+per-batch collectives) strictly in batch order, and return results in batch order with false
+verdicts re-verified by redo."""
+import random
+
+from zebra_amd.dist import run_pipelined_deferred
+
+
+class FakeCtx:
+    def __init__(self, name, clock):
+        self.name, self.clock, self.batch, self.done_at = name, clock, None, None
+
+
+def test_first_ready_harvest_keeps_batch_order():
+    rng = random.Random(5)
+    clock = [0]
+    ctxs = [FakeCtx(i, clock) for i in range(4)]
+    k, bad = 23, {3, 11, 17}
+    launched, harvested, verdicts = [], [], []
+
+    def launch(c):
+        c.batch = len(launched)
+        launched.append(c.batch)
+        c.done_at = clock[0] + rng.randint(1, 12)   # finishes after a random number of polls
+
+    def ready(c):
+        clock[0] += 1
+        return clock[0] >= c.done_at
+
+    def harvest(c):
+        harvested.append(c.batch)
+        return ("part", c.batch), ["sts", c.batch]
+
+    def verdict(part):
+        verdicts.append(part[1])
+        return part[1] not in bad
+
+    res = run_pipelined_deferred(ctxs, k, launch, harvest, verdict, lambda s: ["redo", s], ready=ready)
+    assert launched == list(range(k))
+    assert sorted(harvested) == list(range(k))
+    assert harvested != sorted(harvested)          # out-of-order completion was exercised
+    assert verdicts == list(range(k))              # collectives in batch order
+    for s, (ok, sts) in enumerate(res):
+        assert ok == (s not in bad)
+        assert sts == (["redo", s] if s in bad else ["sts", s])
+
+
+def test_without_ready_harvests_oldest_first():
+    ctxs = [FakeCtx(i, None) for i in range(3)]
+    order = []
+    seq = iter(range(100))
+
+    def launch(c):
+        c.batch = next(seq)
+
+    def harvest(c):
+        order.append(c.batch)
+        return ("p", c.batch), c.batch
+
+    res = run_pipelined_deferred(ctxs, 9, launch, harvest, lambda p: True, lambda s: None)
+    assert order == list(range(9))
+    assert [sts for _, sts in res] == list(range(9))

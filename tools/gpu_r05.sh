@@ -149,13 +149,23 @@ for s in $STEPS; do
       timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs $n --steps 40 > $O/b_$n.json 2> $O/b_$n.err || { echo "bench $n failed"; tail -20 $O/b_$n.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/b_$n.json')); print('shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s', d['config'].get('batches_in_flight_per_gpu'))"
     done ;;
+  hwq8k)
+    # 8k shards (6 in flight) at several hardware-queue counts x stream-pair pools: "Q:P ..."
+    for cfg in ${HWQ:-24:8 16:8 12:6 8:4 32:8}; do
+      q=${cfg%%:*}; pp=${cfg##*:}
+      GPU_MAX_HW_QUEUES=$q ZG_STREAM_PAIRS=$pp ZG_BENCH_HWQ=$q timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs ${HWQN:-8192} --steps 40 > $O/hwq_$q_$pp.json 2> $O/hwq_$q_$pp.err || { echo "bench hwq $cfg failed"; tail -20 $O/hwq_$q_$pp.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/hwq_$q_$pp.json')); print('hwq $cfg', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')"
+    done ;;
+  pipetest)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_multiproc.py tests/test_gpu_rccl.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pipetest.log 2>&1 || { echo "pipeline tests failed"; tail -60 $O/pipetest.log; exit 1; }
+    tail -3 $O/pipetest.log ;;
   k4tests)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_csum.py tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/k4tests.log 2>&1 || { echo "k4 tests failed"; tail -60 $O/k4tests.log; exit 1; }
     tail -3 $O/k4tests.log ;;
   occ8k)
     # 8k shards in flight: wave-time by kernel, resident waves over time, per-stream gaps (tools/occupancy.py)
     cd /tmp && export TMPDIR=/tmp
-    timeout -k 10 300 rocprofv3 --kernel-trace -d $O/occ8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs ${OCCN:-8192} --steps 36 --warmup 6 ${OCCARGS:-} > $O/occ8k.json 2> $O/occ8k.err || { echo "rocprof occ failed"; tail -30 $O/occ8k.err; exit 1; }
-    cd $R && python3 tools/wavetime.py $O/occ8k/run_results.db $O/wavetime_occ.txt > /dev/null && python3 tools/occupancy.py $O/occ8k/run_results.db $O/occupancy.txt && rm -f $O/occ8k/run_results.db && head -12 $O/wavetime_occ.txt ;;
+    timeout -k 10 300 rocprofv3 --kernel-trace ${PROFARGS:-} -d $O/occ8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs ${OCCN:-8192} --steps 36 --warmup 6 ${OCCARGS:-} > $O/occ8k.json 2> $O/occ8k.err || { echo "rocprof occ failed"; tail -30 $O/occ8k.err; exit 1; }
+    cd $R && python3 tools/wavetime.py $O/occ8k/run_results.db $O/wavetime_occ.txt > /dev/null && python3 tools/occupancy.py $O/occ8k/run_results.db $O/occupancy.txt > $O/occupancy_stdout.txt && python3 tools/batch_path.py $O/occ8k/run_results.db $O/batch_path.txt > /dev/null && head -12 $O/occupancy.txt && head -40 $O/batch_path.txt && head -12 $O/wavetime_occ.txt ;;
   esac
 done

@@ -18,6 +18,9 @@ def main():
     db = sqlite3.connect(sys.argv[1])
     cols = [r[1] for r in db.execute("pragma table_info(kernels)").fetchall()]
     sid = next((c for c in ("stream_id", "queue_id", "stream", "queue") if c in cols), None)
+    if "stream_id" in cols and "queue_id" in cols:  # which hardware queue serves each stream
+        pairs = db.execute("select stream_id, queue_id, count(*) from kernels group by stream_id, queue_id").fetchall()
+        print("stream -> queue (kernels): " + ", ".join("%s->%s (%d)" % p for p in sorted(pairs)))
     rows = db.execute("select name, start, end, grid_x * grid_y * grid_z%s from kernels order by start"
                       % (", " + sid if sid else ", 0")).fetchall()
     marks = [r[1] for r in rows if "k_chacha20" in r[0]]

@@ -10,8 +10,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zg.h"
@@ -26,7 +28,12 @@ using namespace zg;
 
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
-#define ZG_NEV 13
+#define ZG_NEV 14  // [13]: zg_gt_check
+// the pinned host block of a context: the root's 576-B Miller partial, the pipeline flags
+// (bfail, fused-wait failure), the K4 entry count, then the n statuses
+#define ZG_PIN_FLAGS 576
+#define ZG_PIN_ENTRIES 584
+#define ZG_PIN_STATUS 640
 #define ZG_NTIMINGS 9
 #define ZG_NSTATS 11
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
@@ -147,6 +154,10 @@ struct zg_ctx {
   // them), or the caller's HBM-resident buffers (zg_batch_begin_device: read in place, no copy)
   const uint8_t *cur_proofs = nullptr, *cur_kinds = nullptr, *cur_inputs = nullptr;
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
+  int eager = 0;             // the pipeline's last steps copied the root partial, flags and statuses to h_pin (ev[4])
+  uint8_t* h_pin = nullptr;  // pinned host memory: ZG_PIN_* layout
+  uint8_t* h_gt = nullptr;   // pinned staging of zg_gt_check (partials in, verdict out; grow-only)
+  size_t h_gt_cap = 0;
   int fused_last = 0;        // the last batch used the fused R-chain + f-chain launch
   int lines_lane = -1;      // ZG_LINES_LANE: -1 auto (the straight-line R-chain from ZG_LINES_LANE_MIN padded
                             // proofs, sized for 1 wave per SIMD when the batch is alone on the device, else
@@ -184,6 +195,19 @@ static int fail(zg_ctx* c, int code, const std::string& msg) {
     hipError_t e_ = (expr);                                                                       \
     if (e_ != hipSuccess) return fail(ctx, ZG_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+// Wait for an event by polling (hipEventQuery + a short sleep) instead of hipEventSynchronize /
+// hipStreamSynchronize: the host loop of batches in flight calls into the runtime from two threads
+// (batch launches / harvests on the main one, the verdicts' final exponentiations on a worker), and
+// a blocking synchronize on one thread held up the other's calls until the GPU work it waited for
+// had finished (8k shards: every relaunch came ~1 ms after the verdict's final exponentiation).
+static hipError_t wait_event(hipEvent_t e) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    std::this_thread::sleep_for(std::chrono::microseconds(10));
+  }
+}
 
 static unsigned nblocks(size_t n) { return (unsigned)((n + ZG_BLOCK - 1) / ZG_BLOCK); }
 
@@ -318,6 +342,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_ok, ZG_NODE_CHUNK));
   A(dalloc(&ctx->d_out, ZG_NODE_CHUNK));
   if (ctx->debug_each) A(dalloc(&ctx->d_dbg, cap));
+  A(hipHostMalloc((void**)&ctx->h_pin, ZG_PIN_STATUS + (size_t)cap, hipHostMallocDefault));
   for (int i = 0; i < ZG_NEV; i++) A(hipEventCreate(&ctx->ev[i]));
   // surface a broken device / stream now rather than inside a later batch
   A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
@@ -351,6 +376,8 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->bn_arena, ctx->d_dbg};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  if (ctx->h_pin) hipHostFree(ctx->h_pin);
+  if (ctx->h_gt) hipHostFree(ctx->h_gt);
   for (int i = 0; i < ZG_NEV; i++)
     if (ctx->ev[i]) hipEventDestroy(ctx->ev[i]);
   set_state(ctx, 0);
@@ -723,8 +750,8 @@ static hipError_t launch_c_tree(zg_ctx* ctx, const BatchBufs& b, hipStream_t st,
 }
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
-  static const int root = 1;
-  HIPCHK(hipMemcpyAsync(ctx->d_nodes, &root, sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+  ctx->eager = 0;
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ctx->d_nodes, 1, 1, ctx->stream));  // node list = {root}
   HIPCHK(hipMemsetAsync(b.bfail, 0, 2 * sizeof(int), ctx->stream));  // bfail, fused-wait failure
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
@@ -764,13 +791,16 @@ static int run_pipeline(zg_ctx* ctx) {
   // auto: fuse only a lone batch whose two grids are resident at once. With other batches in
   // flight on the device the split launches overlap them better (8k shards, 6 in flight: 3.79
   // vs 4.20 ms/batch, profiles/r02i_sweep8k.txt), and a fused grid would share the CUs anyway.
+  // A fused (lone, small) batch is latency-bound: one proof per f-chain lane, 4 rounds per step
+  // instead of the pair step's 6 (config 2: the fused launch 2.95 ms with pairs, r03v). That shape
+  // launches 2 groups blocks (pairs: groups + pgroups), and every block must be resident at once.
+  const bool want_singles = ctx->singles != 0;
+  const unsigned fused_blocks = want_singles ? 2 * groups : groups + pgroups;
   const bool fused = ctx->fuse == 1 ||
-                     (ctx->fuse < 0 && !ctx->fuse_off && groups + pgroups <= (unsigned)ctx->ncu &&
+                     (ctx->fuse < 0 && !ctx->fuse_off && fused_blocks <= (unsigned)ctx->ncu &&
                       ctx->dev->inflight.load(std::memory_order_relaxed) == 0);
   ctx->fused_last = fused;
-  // a fused (lone, small) batch is latency-bound: one proof per f-chain lane, 4 rounds per step
-  // instead of the pair step's 6 (config 2: the fused launch 2.95 ms with pairs, r03v)
-  const bool singles = fused && ctx->singles != 0;
+  const bool singles = fused && want_singles;
   ctx->singles_last = singles;
   // four proofs per lane on large shards (one block per CU from 64k proofs on): 64 Fq2 products
   // per four proofs and step instead of 76 (k_batch_fchain4)
@@ -827,6 +857,21 @@ static int run_pipeline(zg_ctx* ctx) {
   rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
   if (rc) return rc;
   ctx->root_pairs_ready = 1;
+  // the root's Miller partial, the pipeline flags and the statuses go to pinned host memory as the
+  // last steps (ev[4]), so zg_batch_partial / zg_batch_finish find them ready: computed only when
+  // the host asked, the partial serialised the host loop of batches in flight behind a wave that
+  // waited for a whole free SIMD
+  hipLaunchKernelGGL(k_node_partial, dim3(1), dim3(64), 0, ctx->stream, b, nb);
+  hipLaunchKernelGGL(k_f12_to_bytes, dim3(1), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_out, 1, ctx->d_bytes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->h_pin, ctx->d_bytes, 576, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + ZG_PIN_FLAGS, ctx->d_int + 8, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + ZG_PIN_ENTRIES, ctx->msm.start + msm_shape(ctx->npad).ncount(), sizeof(int),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  if (ctx->n)
+    HIPCHK(hipMemcpyAsync(ctx->h_pin + ZG_PIN_STATUS, ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  ctx->eager = 1;
   return ZG_OK;
 }
 
@@ -974,11 +1019,9 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
 // the fused shape off for this context)
 static int collect_batch_stats(zg_ctx* ctx) {
   int flags[2] = {0, 0}, entries = 0;
-  HIPCHK(hipMemcpyAsync(flags, ctx->d_int + 8, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipMemcpyAsync(&entries, ctx->msm.start + msm_shape(ctx->npad).ncount(), sizeof(int),
-                        hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
-  HIPCHK(hipEventSynchronize(ctx->ev[4]));
+  HIPCHK(wait_event(ctx->ev[4]));  // the pipeline's last step (run_pipeline)
+  memcpy(flags, ctx->h_pin + ZG_PIN_FLAGS, sizeof(flags));
+  memcpy(&entries, ctx->h_pin + ZG_PIN_ENTRIES, sizeof(int));
   ctx->stats[0]++;
   if (ctx->fused_last) ctx->stats[1]++;
   if (ctx->quads_last) ctx->stats[7]++;
@@ -1007,25 +1050,49 @@ extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
   std::lock_guard<std::mutex> g(ctx->mu);
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_partial before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
-  std::vector<int> root = {1};
-  int rc = check_nodes(ctx, root, 1, nullptr, partial);
-  if (rc) return rc;
+  if (!ctx->eager) return fail(ctx, ZG_E_STATE, "zg_batch_partial: no pipeline result");
+  HIPCHK(wait_event(ctx->ev[4]));
+  memcpy(partial, ctx->h_pin, 576);
   return collect_batch_stats(ctx);
+}
+
+extern "C" int zg_batch_ready(zg_ctx* ctx) {
+  if (!ctx) return ZG_E_INVAL;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->state != 1 || !ctx->eager) return fail(ctx, ZG_E_STATE, "zg_batch_ready before zg_batch_begin");
+  HIPCHK(hipSetDevice(ctx->device));
+  const hipError_t e = hipEventQuery(ctx->ev[4]);
+  if (e == hipErrorNotReady) return 0;
+  HIPCHK(e);
+  return 1;
 }
 
 extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok) {
   if (!ctx || !partials || !ok || count == 0 || count > ZG_NODE_CHUNK) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipMemcpyAsync(ctx->d_bytes, partials, 576 * count, hipMemcpyHostToDevice, ctx->stream));
+  // pinned staging (asynchronous copies), then a polling wait (wait_event)
+  const size_t need = 576 * count + 64;
+  if (ctx->h_gt_cap < need) {
+    if (ctx->h_gt) HIPCHK(hipHostFree(ctx->h_gt));
+    ctx->h_gt = nullptr;
+    ctx->h_gt_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&ctx->h_gt, need, hipHostMallocDefault));
+    ctx->h_gt_cap = need;
+  }
+  memcpy(ctx->h_gt, partials, 576 * count);
+  HIPCHK(hipMemcpyAsync(ctx->d_bytes, ctx->h_gt, 576 * count, hipMemcpyHostToDevice, ctx->stream));
   hipLaunchKernelGGL(k_f12_from_bytes, dim3(nblocks(count)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_bytes, (int)count,
                      ctx->d_pairf);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(64), 0, ctx->stream, ctx->d_pairf, (int)count, ctx->d_ok,
                      ctx->d_out);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(ok, ctx->d_ok, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int* hok = (int*)(ctx->h_gt + 576 * count);
+  HIPCHK(hipMemcpyAsync(hok, ctx->d_ok, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[13], ctx->stream));
+  HIPCHK(wait_event(ctx->ev[13]));
+  *ok = *hok;
   return ZG_OK;
 }
 
@@ -1148,8 +1215,13 @@ static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool 
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_finish before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
   std::vector<uint8_t> st(ctx->n);
-  if (ctx->n) HIPCHK(hipMemcpyAsync(st.data(), ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->eager && batch_ok) {  // the pipeline's own status copy (run_pipeline, ev[4])
+    HIPCHK(wait_event(ctx->ev[4]));
+    if (ctx->n) memcpy(st.data(), ctx->h_pin + ZG_PIN_STATUS, ctx->n);
+  } else {
+    if (ctx->n) HIPCHK(hipMemcpyAsync(st.data(), ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
   if (!batch_ok) {
     int rc = bisect(ctx, st, root_failed);
     if (rc) {
@@ -1646,6 +1718,7 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
   // one batch check per chunk of at most ZG_PGHR_CHUNK proofs: the call's arena (~27 KB per proof,
   // mostly the b lines) stays bounded at the chunk size however large the caller's window is
   if (kernel_ms) *kernel_ms = 0;
+  bool any_failed = false;
   for (size_t o = 0; o < n; o += ZG_PGHR_CHUNK) {
     const size_t m = n - o < ZG_PGHR_CHUNK ? n - o : ZG_PGHR_CHUNK;
     bool batch_failed = false;
@@ -1656,8 +1729,11 @@ extern "C" int zg_pghr13_verify(zg_ctx* ctx, size_t n, const uint8_t* proofs, co
                                     &ctx->err);
     if (rc != ZG_OK) return rc;
     if (kernel_ms) *kernel_ms += ms;
+    any_failed = any_failed || batch_failed;
+  }
+  if (n) {  // once per call, however many chunks it took (include/zg.h zg_stats [8], [9])
     ctx->stats[8]++;
-    if (batch_failed) ctx->stats[9]++;
+    if (any_failed) ctx->stats[9]++;
   }
   return ZG_OK;
 }

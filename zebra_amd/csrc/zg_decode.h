@@ -34,10 +34,16 @@ namespace zg {
 // point goes to ptAC (inf = the point did not decode).
 //
 // k_decode_points: one wave per (64 proofs, job), the jobs of a decoded point being independent
-// of each other: blocks [0, G) the GLV products [r_i] A_i (to affine -> ptA); blocks [G, 3G)
-// alternate the G1 subgroup checks of A and C (sigma(P) = -[x^2] P -> okbits); blocks
-// [3G, 4G) decompress B (Fq2 sqrt; its G2 subgroup check rides on k_batch_lines). C needs no
-// per-proof scalar product: sum r_i C_i is K4's Pippenger MSM (zg_msm.h) on the side stream.
+// of each other. Two grid layouts (G = npad / 64 groups of 64 proofs):
+//   K4 (cglv = 0: shards from ZG_K4_MIN padded proofs, or any batch with others in flight):
+//     blocks [0, G) the GLV products [r_i] A_i (to affine -> ptA); [G, 3G) alternate the G1
+//     subgroup checks of A and C (sigma(P) = -[x^2] P -> okbits); [3G, 4G) decompress B (Fq2
+//     sqrt; its G2 subgroup check rides on k_batch_lines). C needs no per-proof scalar product:
+//     sum r_i C_i is K4's Pippenger MSM (zg_msm.h) on the side stream.
+//   GLV C sums (cglv = 1: a lone batch below ZG_K4_MIN): blocks [0, G) [r_i] A_i as above,
+//     [G, 2G) the GLV products [r_i] C_i into the C-sum tree leaves ctree[npad + i] (the proof's
+//     key; infinity for the other keys), which the side stream sums up the tree (k_tree_c); the
+//     subgroup checks move to [2G, 4G) and B to [4G, 5G).
 // The heavy waves are dispatched first, two per SIMD (ZG_DECODE_WPE), and the B waves fill the
 // tail. The scalar products run before the statuses are known (a point that did not decode
 // skips its own; the rest are masked by k_decode_finish).

@@ -20,7 +20,8 @@ hipError_t launch_decode_sqrt(unsigned groups, hipStream_t st, const BatchBufs& 
 
 // G1 square roots, then the point jobs (GLV r_i A_i, subgroup checks, B), then per-proof statuses and Fr leaves
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv) {
-  launch_decode_sqrt(groups, st, b);
+  const hipError_t e = launch_decode_sqrt(groups, st, b);
+  if (e != hipSuccess) return e;
   static const int split = getenv("ZG_DECODE_SPLIT") ? atoi(getenv("ZG_DECODE_SPLIT")) : 0;
   const unsigned nglv = cglv ? 2 * groups : groups;
   if (split) {

@@ -705,6 +705,22 @@ __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int
   if (threadIdx.x == 0) nb.ok[idx] = one ? 1 : 0;
 }
 
+// The batch root's Miller partial (k_node_final mode 1 for node 1) as the pipeline's last step,
+// with the registers of coop products only: k_node_final's final-exponentiation path needs a whole
+// SIMD (512 registers), and in flight such a wave waited milliseconds for one -- the host loop
+// waited on it for every batch (8k shards, 6 in flight: 2.3 of 2.7 ms per batch).
+__global__ void __launch_bounds__(64) k_node_partial(BatchBufs b, NodeBufs nb) {
+  __shared__ CoopWS ws;
+  coop_init(&ws);
+  coop_load(&ws, 0, b.ftree[1]);
+  const int npn = b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS;
+  for (int p = 0; p < npn; p++) {
+    coop_load(&ws, 1, nb.pairf[p]);
+    coop_mul(&ws, 0, 0, 1);
+  }
+  coop_store(&ws, 0, nb.out[0]);
+}
+
 // K7 across ranks: product of partials, ONE final exponentiation (one wave), == 1 ?
 __global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
   __shared__ CoopWS ws;

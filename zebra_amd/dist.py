@@ -80,32 +80,46 @@ def run_pipelined(ctxs, k, launch, complete):
     return out
 
 
-def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo):
+def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None):
     """run_pipelined with the verdict taken off the context's critical path.
 
     harvest(ctx) -> (partial, statuses) waits for a batch's Miller partial and reads its
     per-proof statuses as if the batch verdict were true (decode rejects and input-count
     errors are final either way); the context is then free and is relaunched at once.
-    verdict(partial) -> bool (the all-gather + ONE final exponentiation, on a checker context
-    of its own) runs on a single worker thread in batch order, so the per-batch collectives
-    line up across ranks exactly as in run_pipelined. A batch whose verdict is false is
-    re-verified by redo(batch_index) -> statuses (bisection on a fresh pass: per-proof
-    results do not depend on the batch scalars) after the pipeline has drained. Returns the k
-    (verdict, statuses) pairs in batch order; all verdicts are in before it returns."""
+    ready(ctx) -> bool (optional; Context.batch_ready, never blocks): batches in flight finish out
+    of launch order (they share the device), so the loop harvests whichever batch is done first
+    and relaunches its context, instead of idling finished contexts behind the oldest batch
+    (without `ready`: strictly the oldest). verdict(partial) -> bool (the all-gather + ONE final
+    exponentiation, on a checker context of its own) runs on a single worker thread in BATCH order
+    whatever the harvest order, so the per-batch collectives line up across ranks exactly as in
+    run_pipelined. A batch whose verdict is false is re-verified by redo(batch_index) -> statuses
+    (bisection on a fresh pass: per-proof results do not depend on the batch scalars) after the
+    pipeline has drained. Returns the k (verdict, statuses) pairs in batch order; all verdicts are
+    in before it returns."""
+    import time
     from concurrent.futures import ThreadPoolExecutor
-    pend, q = [], []
+    free, inflight = list(ctxs), []   # inflight: (batch index, ctx) in launch order
+    done, res = {}, {}                # harvested, verdict not yet submitted / submitted
+    nxt = launched = 0
     with ThreadPoolExecutor(max_workers=1) as ex:
-        def take():
-            s, c = q.pop(0)
-            part, sts = harvest(c)
-            pend.append((s, sts, ex.submit(verdict, part)))
-        for s in range(k):
-            if len(q) == len(ctxs):
-                take()
-            c = ctxs[s % len(ctxs)]
-            launch(c)
-            q.append((s, c))
-        while q:
-            take()
-        oks = [f.result() for _, _, f in pend]
-    return [(ok, sts if ok else redo(s)) for ok, (s, sts, _) in zip(oks, pend)]
+        while launched < k or inflight:
+            while free and launched < k:
+                c = free.pop(0)
+                launch(c)
+                inflight.append((launched, c))
+                launched += 1
+            i = 0
+            if ready is not None:
+                i = next((j for j, (_, c) in enumerate(inflight) if ready(c)), None)
+                if i is None:          # nothing finished yet: poll again shortly
+                    time.sleep(2e-5)
+                    continue
+            s, c = inflight.pop(i)
+            done[s] = harvest(c)
+            free.append(c)
+            while nxt in done:         # verdicts (collectives) strictly in batch order
+                part, sts = done.pop(nxt)
+                res[nxt] = (sts, ex.submit(verdict, part))
+                nxt += 1
+        oks = [res[s][1].result() for s in range(k)]
+    return [(ok, res[s][0] if ok else redo(s)) for s, ok in enumerate(oks)]

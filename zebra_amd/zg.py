@@ -62,6 +62,7 @@ def lib():
         L.zg_batch_begin.argtypes = [vp, sz, u8p, u8p, u8p, u8p, u8p]
         L.zg_batch_begin_device.argtypes = [vp, sz, vp, vp, vp, vp, vp]
         L.zg_batch_partial.argtypes = [vp, u8p]
+        L.zg_batch_ready.argtypes = [vp]
         L.zg_gt_check.argtypes = [vp, sz, u8p, ctypes.POINTER(i)]
         L.zg_batch_finish.argtypes = [vp, i, u8p]
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
@@ -271,6 +272,13 @@ class Context:
         out = ctypes.create_string_buffer(GT_BYTES)
         self._chk(lib().zg_batch_partial(self._p, out))
         return out.raw
+
+    def batch_ready(self):
+        """True once the batch's device work is done (never blocks; zg_batch_ready)"""
+        r = lib().zg_batch_ready(self._p)
+        if r < 0:
+            self._chk(r)
+        return r == 1
 
     def gt_check(self, partials):
         ok = ctypes.c_int(0)
