@@ -43,13 +43,16 @@ assert W_DECODE + W_K4 + W_LINES + W_FCHAIN + W_TREE == W_TOTAL
 # K4 bucket phase, algorithmic HBM bytes: per entry the 4-byte bucket entry and the 100-byte
 # affine C_i it names (G1A), plus the bucket offsets read and the (T, U) segment sums written
 # (Jacobian, 144 B each) -- zg_msm.h msm_shape: c = 11 from 32k padded proofs, 10 from 8k, 9 below
-K4_ENTRY_BYTES = 4 + 100
+# K4's bucket phase per entry: the 4-B entry + its C_i operands as lazy digits (x or beta x, y:
+# 2 x 14 x 4 B, written once per proof by k_msm_count); per segment the (T, U) pair written as
+# G1D (3 x 14 words each); the isolated pass runs a lone batch, so P = 4 (2 below 8k) lanes per bucket
+K4_ENTRY_BYTES = 4 + 2 * 56
 
 
 def k4_fixed_bytes(npad):
     c, w, nb, parts = (11, 6, 1024, 4) if npad >= 32768 else (10, 7, 512, 4) if npad >= 8192 else (9, 8, 256, 2)
     ncount = 3 * w * nb
-    return ncount * 4 + (ncount // (64 // parts)) * 2 * 144
+    return ncount * 4 + (ncount // (64 // parts)) * 2 * 168
 NOMINAL_LANES = 256 * 4 * 16                        # MI355X: CUs x SIMDs x lanes per clock
 MACS_PER_FQMUL = 288                                # 2 * 12^2 32x32->64 MACs (product + CIOS reduction)
 
@@ -478,7 +481,7 @@ def main():
               "frac": k4_bytes / (iso_avg[8] * 1e-3) / 8e12, "traffic": k4_traffic,
               "k4_total_ms": iso_avg[7],
               "note": "HBM GB/s of the Pippenger bucket phase (isolated pass, HIP events around "
-                      "k_msm_bucket): entries x (4-B entry + 100-B affine C_i) + partial sums written; "
+                      "k_msm_bucket): entries x (4-B entry + 112-B digit operands of C_i) + segment sums written; "
                       "the phase is VALU-bound (mixed additions), not HBM-bound"}
     out = {
         "metric": "Sapling Groth16 proofs verified/sec (batch 64k) at 1/2/4/8 MI355X",

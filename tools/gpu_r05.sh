@@ -166,6 +166,6 @@ for s in $STEPS; do
     # 8k shards in flight: wave-time by kernel, resident waves over time, per-stream gaps (tools/occupancy.py)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace ${PROFARGS:-} -d $O/occ8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs ${OCCN:-8192} --steps 36 --warmup 6 ${OCCARGS:-} > $O/occ8k.json 2> $O/occ8k.err || { echo "rocprof occ failed"; tail -30 $O/occ8k.err; exit 1; }
-    cd $R && python3 tools/wavetime.py $O/occ8k/run_results.db $O/wavetime_occ.txt > /dev/null && python3 tools/occupancy.py $O/occ8k/run_results.db $O/occupancy.txt > $O/occupancy_stdout.txt && python3 tools/batch_path.py $O/occ8k/run_results.db $O/batch_path.txt > /dev/null && head -12 $O/occupancy.txt && head -40 $O/batch_path.txt && head -12 $O/wavetime_occ.txt ;;
+    cd $R && python3 tools/wavetime.py $O/occ8k/run_results.db $O/wavetime_occ.txt > /dev/null && python3 tools/occupancy.py $O/occ8k/run_results.db $O/occupancy.txt > $O/occupancy_stdout.txt && python3 tools/batch_path.py $O/occ8k/run_results.db $O/batch_path.txt > /dev/null && head -12 $O/occupancy.txt && head -40 $O/batch_path.txt && head -12 $O/wavetime_occ.txt && { [ -z "${PROFARGS:-}" ] || python3 tools/host_api.py $O/occ8k/run_results.db $O/host_api.txt > /dev/null; } && { [ -n "${KEEPDB:-}" ] || rm -f $O/occ8k/run_results.db; } ;;
   esac
 done

@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+// (the lazy-digit products stay out of line, zg_fqd.h ZG_FQD_CALL = 1: inlined, k_msm_bucket drops
+// its 8-B call frame and runs 0.89 -> 0.82 ms isolated at 64k, but k_msm_group's 39 k inlined
+// instructions take its window-doubling chain -- K4's critical path -- from ~0.9 to 1.3 ms;
+// profiles/r05l_kernel_stats_iso_k4_inline.csv)
+
 #include "../../include/zg.h"
 #include "zg_msm.h"
 
