@@ -94,3 +94,43 @@ def test_glv_tree_exact_reject_set_with_deferred_b(work4k):
         assert st["bisections"] == 1 and st["b_subgroup_recomputes"] >= 1
     assert got["glv"] == want
     assert got["k4"] == want
+
+
+def _ctx_env(env, n):
+    from zebra_amd import Context
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return Context(device=0, max_batch=n)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("env", [{"ZG_SERIAL_SIDE": 1}, {"ZG_TREE_COOP_BELOW": 1}, {"ZG_TREE_COOP_BELOW": 1 << 30},
+                                 {"ZG_FCHAIN_SINGLE": 0}, {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1},
+                                 {"ZG_LINES_FCHAIN": 0, "ZG_LINES_LANE": 1}, {"ZG_K4_MIN": 1}],
+                         ids=lambda e: ",".join("%s=%s" % kv for kv in e.items()))
+def test_context_knobs_give_the_same_partial(work4k, env):
+    """every per-context schedule switch (zg.hip zg_create: side work serialised on the main stream,
+    product-tree levels lane-per-node or wave-per-node, the fused launch with proof pairs instead of
+    single proofs, split quads, the straight-line R-chain, K4 on a lone small batch) computes the
+    same batch: byte-identical 576-B Miller partial to the default schedule's for seeded scalars"""
+    n = 2048
+    proofs, kinds, inputs = work4k
+    proofs, kinds, inputs = proofs[:192 * n], kinds[:n], inputs[:288 * n]
+    r = random.Random(77).randbytes(16 * n)
+    parts = []
+    for e in ({}, env):
+        c = _ctx_env(e, n)
+        try:
+            c.batch_begin(proofs, kinds, inputs, r=r)
+            parts.append(c.batch_partial())
+            assert c.gt_check([parts[-1]])
+            assert c.batch_finish(True, n) == [0] * n
+        finally:
+            c.close()
+    assert parts[0] == parts[1]

@@ -31,11 +31,6 @@ for s in $STEPS; do
       timeout -k 10 60 ./$v 65536 3 >> $O/mb.txt 2>&1 || { echo "mb $v failed"; tail -20 $O/mb.txt; exit 1; }
     done
     cat $O/mb.txt ;;
-  decsplit)
-    # the decode jobs as separate launches (ZG_DECODE_SPLIT=1), serial side stream, kernel stats
-    cd /tmp && export TMPDIR=/tmp
-    ZG_DECODE_SPLIT=1 ZG_SERIAL_SIDE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_dec -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --steps 4 --warmup 0 --inflight 1 --sync-verdict > $O/prof_dec.json 2> $O/prof_dec.err || { echo "rocprof decsplit failed"; tail -30 $O/prof_dec.err; exit 1; }
-    cd $R && python3 tools/rocpd_stats.py $O/prof_dec/run_results.db $O/kernel_stats_decsplit.csv && rm -f $O/prof_dec/run_results.db && head -14 $O/kernel_stats_decsplit.csv ;;
   lanetest)
     timeout -k 10 400 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_parity.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/lanetest.log 2>&1 || { echo "lane tests failed"; tail -40 $O/lanetest.log; exit 1; }
     tail -3 $O/lanetest.log ;;
@@ -159,6 +154,10 @@ for s in $STEPS; do
   pipetest)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_multiproc.py tests/test_gpu_rccl.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/pipetest.log 2>&1 || { echo "pipeline tests failed"; tail -60 $O/pipetest.log; exit 1; }
     tail -3 $O/pipetest.log ;;
+  mbaff)
+    # affine vs projective R-chain step cost (tools/mb_affine.hip, built on the CPU side)
+    timeout -k 10 120 ./tools/mb_affine 65536 16 > $O/mb_affine.txt 2>&1 || { echo "mb_affine failed"; cat $O/mb_affine.txt; exit 1; }
+    cat $O/mb_affine.txt ;;
   k4tests)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_csum.py tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/k4tests.log 2>&1 || { echo "k4 tests failed"; tail -60 $O/k4tests.log; exit 1; }
     tail -3 $O/k4tests.log ;;

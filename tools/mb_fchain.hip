@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
   for (uint32_t w : h) hash = (hash ^ w) * 0x100000001b3ull;
   int hf[2];
   CK(hipMemcpy(hf, bfail, 8, hipMemcpyDeviceToHost));
-  if (hf[1]) printf("dataflow wait gave up (bfail[1] = %d)\n", hf[1]);
+  if (hf[1]) printf("bfail[1] = %d\n", hf[1]);
   const double macs = 5192.0 * 288.0 * n;
   printf("fchain4 n=%d blocks=%u: best %.3f ms, mean %.3f ms, %.2f T alg-MAC/s, nodes hash %016llx\n", n, blocks, best,
          sum / reps, macs / (best * 1e-3) / 1e12, (unsigned long long)hash);

@@ -811,114 +811,6 @@ def check_lazy(specs, trials=40):
                 assert env["v"] == val(f) and all(c < P for c in env["v"]), (name, j)
 
 
-# ---------------------------------------------------------------- dataflow tables (f-chain)
-# The f-chain programs can also run without a barrier per round (zg_prog.h prog_run_df): every wave
-# walks its own column of the schedule, and LDS counters per slot, reset at every step, order the
-# accesses -- wv[s] counts the writes to slot s so far in the step, rd[s] the (product, slot) reads.
-# A product waits until each operand slot holds the version it reads (RAW: wv[s] >= that atom's write
-# index, 0 for a program input), bumps rd[s] once per distinct slot after its loads, waits until every
-# read of the slot's previous occupants is done before it overwrites dst (WAR: rd[dst] >= the reads
-# of all earlier versions), then stores and bumps wv[dst]. Every wait points at a product of an
-# earlier round or at a same-round read, so the per-wave round order cannot deadlock (df_simulate).
-DF_PROGS = ("q4sq", "q4")
-
-
-def df_tables(prog, outs, sch):
-    """per product: (raw [(slot, need)], reads [slot], (dst, war_need)) in product index order"""
-    slot, rnd = sch["slot"], sch["rnd"]
-    n = len(prog.prods)
-    order = sorted(range(n), key=lambda i: (rnd[i], i))
-    # write index of every product atom in its slot (1-based, in round order)
-    wcount, widx = {}, {}
-    for i in order:
-        sl = slot[("p", i)]
-        assert not isinstance(sl, tuple), "f-chain programs have no HBM sinks"
-        wcount[sl] = wcount.get(sl, 0) + 1
-        widx[i] = wcount[sl]
-    # readers of each version: version (slot, w) -> distinct reading products
-    readers = {}
-    for i in range(n):
-        L, R, _ = prog.prods[i]
-        for k in set(list(L) + list(R)):
-            sl = slot[k]
-            ver = 0 if k[0] == "in" else widx[k[1]]
-            readers.setdefault((sl, ver), set()).add(i)
-    out = []
-    for i in range(n):
-        L, R, _ = prog.prods[i]
-        need = {}
-        for k in set(list(L) + list(R)):
-            sl = slot[k]
-            ver = 0 if k[0] == "in" else widx[k[1]]
-            need[sl] = max(need.get(sl, 0), ver)
-        dst = slot[("p", i)]
-        war = sum(len(readers.get((dst, v), ())) for v in range(widx[i]))
-        # one slot read per distinct slot: two versions of one slot in one product cannot happen
-        assert all(len({(0 if k[0] == "in" else widx[k[1]]) for k in set(list(L) + list(R)) if slot[k] == sl}) == 1
-                   for sl in need), (prog.name, i)
-        out.append((sorted(need.items()), sorted(need), (dst, war)))
-    return out
-
-
-def df_simulate(prog, outs, sch, nw, trials=200):
-    """run the dataflow protocol with random interleavings of the waves' columns on an LDS model:
-    no deadlock, and the outputs equal the reference values"""
-    rng = random.Random(5)
-    tab = df_tables(prog, outs, sch)
-    for t in range(trials):
-        vals = [(rng.randrange(P), rng.randrange(P)) for _ in prog.inputs]
-        lds = {sch["slot"][("in", i)]: v for i, v in enumerate(vals)}
-        wv, rd = {}, {}
-        cols = [[i for r in sch["rounds"] for i in [r[w] if w < len(r) else None] if i is not None] for w in range(nw)]
-        pos = [0] * nw
-        pend = {}  # wave -> (phase, data)
-        steps = 0
-        while any(pos[w] < len(cols[w]) for w in range(nw)):
-            steps += 1
-            assert steps < 100000, "deadlock"
-            w = rng.randrange(nw)
-            if pos[w] >= len(cols[w]):
-                continue
-            i = cols[w][pos[w]]
-            raw, reads, (dst, war) = tab[i]
-            ph = pend.get(w, (0, None))
-            if ph[0] == 0:  # RAW
-                if all(wv.get(sl, 0) >= nd for sl, nd in raw):
-                    L, R, kind = prog.prods[i]
-
-                    def ev(f):
-                        r0 = r1 = 0
-                        for k, (c0, c1) in f.items():
-                            x0, x1 = lds[sch["slot"][k]]
-                            r0 += c0 * x0 - c1 * x1
-                            r1 += c0 * x1 + c1 * x0
-                        return (r0 % P, r1 % P)
-                    x, y = ev(L), ev(R)
-                    if kind == K_MULC0:
-                        y = (y[0], 0)
-                    elif kind == K_MULC1:
-                        y = (y[1], 0)
-                    for sl in reads:
-                        rd[sl] = rd.get(sl, 0) + 1
-                    z = ((x[0] * y[0] - x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)
-                    pend[w] = (1, z)
-            else:  # WAR, then write
-                if rd.get(dst, 0) >= war:
-                    lds[dst] = ph[1]
-                    wv[dst] = wv.get(dst, 0) + 1
-                    pend[w] = (0, None)
-                    pos[w] += 1
-
-        def evo(f):
-            r0 = r1 = 0
-            for k, (c0, c1) in f.items():
-                x0, x1 = lds[sch["slot"][k]]
-                r0 += c0 * x0 - c1 * x1
-                r1 += c0 * x1 + c1 * x0
-            return (r0 % P, r1 % P)
-        assert [evo(f) for f in outs] == reference(prog, outs, vals), (prog.name, t)
-
-
 def emit(specs):
     out = ["// GENERATED by zebra_amd/csrc/gen_prog.py -- do not edit.", "#pragma once",
            "// included by zg_prog.h (needs AtomSpace and the Fq2 helpers)", "namespace zg {"]
@@ -988,25 +880,6 @@ def emit(specs):
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
                          ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
-    # dataflow tables (DF_PROGS; other products: no entries)
-    raw_off, raw, rd_off, rdl, war = [0], [], [0], [], []
-    for name, prog, outs, nw, sch in specs:
-        tab = df_tables(prog, outs, sch) if name in DF_PROGS else [([], [], (0, 0))] * len(prog.prods)
-        for rw, reads, (dst, wn) in tab:
-            raw += [(sl << 8) | nd for sl, nd in rw if nd > 0]  # a program input is always there
-            raw_off.append(len(raw))
-            rdl += list(reads)
-            rd_off.append(len(rdl))
-            assert wn < 1 << 16 and dst < 256
-            war.append((dst << 16) | wn)
-    out.append("// dataflow tables of the f-chain programs (gen_prog.py df_tables): per global product gk,")
-    out.append("// DF_RAW[DF_RAW_OFF[gk] ..) = slot << 8 | writes needed, DF_RD[DF_RD_OFF[gk] ..) = slots read,")
-    out.append("// DF_WAR[gk] = dst << 16 | reads of dst's earlier versions needed before the store")
-    out.append("__device__ __constant__ const uint16_t DF_RAW_OFF[%d] = {%s};" % (len(raw_off), ", ".join(map(str, raw_off))))
-    out.append("__device__ __constant__ const uint16_t DF_RAW[%d] = {%s};" % (max(1, len(raw)), ", ".join(map(str, raw or [0]))))
-    out.append("__device__ __constant__ const uint16_t DF_RD_OFF[%d] = {%s};" % (len(rd_off), ", ".join(map(str, rd_off))))
-    out.append("__device__ __constant__ const uint8_t DF_RD[%d] = {%s};" % (max(1, len(rdl)), ", ".join(map(str, rdl or [0]))))
-    out.append("__device__ __constant__ const uint32_t DF_WAR[%d] = {%s};" % (len(war), ", ".join(map(str, war))))
     out.append("// operands of global product gk; returns the product kind (f2_mul_kind)")
     out.append("__device__ __forceinline__ int prog_operands(int gk, const AtomSpace& at, Fq2& x, Fq2& y, int& dst) {")
     out.append("  switch (gk) {")
@@ -1083,9 +956,6 @@ if __name__ == "__main__":
         json.dump({name: sch["rounds"] for name, prog, outs, nw, sch in specs if name in SEARCH},
                   open(SCHED_CACHE, "w"), indent=0)
     selfcheck(specs)
-    for name, prog, outs, nw, sch in specs:
-        if name in DF_PROGS:
-            df_simulate(prog, outs, sch, nw)
     if LAZY:
         check_lazy(specs)
     for name, prog, outs, nw, sch in specs:

@@ -63,9 +63,9 @@ __global__ void __launch_bounds__(64, ZG_DECODE_SQRT_WPE) k_decode_sqrt(BatchBuf
 }
 #else
 
-// JOB < 0: every job in one launch (grid 4G); JOB = 0 / 1 / 2: that job alone (grid G / 2G / G,
-// ZG_DECODE_SPLIT=1: separate launches, so each job gets its own register budget and its own
-// kernel-trace line)
+// JOB < 0: every job in one launch (grid 4G, the product's only launch); JOB = 0 / 1 / 2: that job
+// alone (grid G / 2G / G: round 4's per-job profiles, profiles/r04b_kernel_stats_decode_split.csv,
+// compiled only by tooling)
 // cglv (small shards, ZG_K4_MIN): the GLV products r_i C_i run here too, as blocks [G, 2G) beside
 // those of A, and go to the C-sum tree leaves (ctree[npad + i], the proof's key; the other keys'
 // entries the point at infinity) -- the side stream then sums them by the tree levels instead of

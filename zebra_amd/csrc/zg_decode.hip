@@ -22,15 +22,8 @@ hipError_t launch_decode_sqrt(unsigned groups, hipStream_t st, const BatchBufs& 
 hipError_t launch_batch_decode(unsigned groups, hipStream_t st, const BatchBufs& b, int cglv) {
   const hipError_t e = launch_decode_sqrt(groups, st, b);
   if (e != hipSuccess) return e;
-  static const int split = getenv("ZG_DECODE_SPLIT") ? atoi(getenv("ZG_DECODE_SPLIT")) : 0;
   const unsigned nglv = cglv ? 2 * groups : groups;
-  if (split) {
-    hipLaunchKernelGGL(k_decode_points<0>, dim3(nglv), dim3(64), 0, st, b, cglv);
-    hipLaunchKernelGGL(k_decode_points<1>, dim3(2 * groups), dim3(64), 0, st, b, cglv);
-    hipLaunchKernelGGL(k_decode_points<2>, dim3(groups), dim3(64), 0, st, b, cglv);
-  } else {
-    hipLaunchKernelGGL(k_decode_points<-1>, dim3(nglv + 3 * groups), dim3(64), 0, st, b, cglv);
-  }
+  hipLaunchKernelGGL(k_decode_points<-1>, dim3(nglv + 3 * groups), dim3(64), 0, st, b, cglv);
   hipLaunchKernelGGL(k_decode_finish, dim3(groups), dim3(64), 0, st, b);
   return hipGetLastError();
 }

@@ -302,11 +302,6 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
   };
   if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
   load_lines(0);
-#if ZG_FC_DF
-  __shared__ int df_cnt[64];
-  bool df_ok = true;
-  if (wave == 7) df_cnt[lane] = 0;
-#endif
   __syncthreads();
   int n = 0;
   for (int i = ZG_XH_TOP;; i--) {
@@ -315,12 +310,7 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_Q4 : ZG_PROG_Q4SQ);
       ZG_TRACE_S(n, 0);
-#if ZG_FC_DF
-      df_ok &= prog_run_df(pid, at, df_cnt);
-      __syncthreads();
-#else
       prog_run<true>(pid, at);
-#endif
       ZG_TRACE_S(n, 1);
       Fq2 v;
       if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
@@ -329,9 +319,6 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
       ZG_TRACE_S(n, 3);
       n++;
       if (wave < 6) at.put(wave, v);
-#if ZG_FC_DF
-      if (wave == 7) df_cnt[lane] = 0;
-#endif
       if (n < ZG_NCOEFF) load_lines(n);
       ZG_TRACE_S(n - 1, 4);
       __syncthreads();
@@ -339,9 +326,6 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     }
     if (last) break;
   }
-#if ZG_FC_DF
-  if (!df_ok && (threadIdx.x & 63) == 0) atomicOr(&b.bfail[1], 2);  // broken dataflow invariant
-#endif
   // conjugate (u < 0) and store the quad node
   if (wave < 6 && inb) {
     Fq2 v = at.get(wave);
