@@ -459,9 +459,13 @@ def main():
     if not iso:
         iso = timings
     fused = iso[0][1] < 0.05   # the fused launch leaves the lines phase empty (isolated pass)
-    quads = ctx.stats().get("quad_fchain_launches", 0) > 0  # four proofs per lane (k_batch_fchain4)
+    st0 = ctx.stats()
+    quads = st0.get("quad_fchain_launches", 0) > 0  # four proofs per lane (k_batch_fchain4)
+    # group line products (k_line_prod) + one chain per group (k_batch_fchaing): the f-chain phase
+    # is the two launches back to back; the work stays the frozen per-proof Miller-loop count
+    lprod = st0.get("line_product_batches", 0) > 0
     rk, wk = ("k_lines_fchain", W_LINES + W_FCHAIN) if fused else \
-        ("k_batch_fchain4" if quads else "k_batch_fchain", W_FCHAIN)
+        ("k_line_prod+k_batch_fchaing" if lprod else "k_batch_fchain4" if quads else "k_batch_fchain", W_FCHAIN)
     achieved = wk * MACS_PER_FQMUL * shard / (avg[2] * 1e-3)
     iso_avg = [sum(t[i] for t in iso) / len(iso) for i in range(NP)]
     iso_achieved = wk * MACS_PER_FQMUL * shard / (iso_avg[2] * 1e-3)

@@ -303,7 +303,9 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * took), [9] those in which a chunk's batch check failed (that chunk then ran the per-proof check
  * for the exact statuses), [10] batches whose sums r_i C_i came
  * from the GLV products in decode and the C-sum tree (shards below 16,384 padded proofs -- ZG_K4_MIN
- * -- instead of K4's Pippenger buckets; [6] is 0 for them). Writes min(n, 11) values, zero beyond. */
+ * -- instead of K4's Pippenger buckets; [6] is 0 for them), [11] of the four-proofs-per-lane batches
+ * ([7]) those whose f-chain ran as group line products + one chain per group (k_line_prod,
+ * k_batch_fchaing; ZG_LINE_GROUP proofs a group). Writes min(n, 12) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

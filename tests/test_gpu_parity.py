@@ -133,14 +133,19 @@ def test_batch_4096_one_percent_corrupted(ctx):
     assert sts == want
 
 
-def test_batch_4096_corrupted_quad_fchain(ctx, monkeypatch):
+@pytest.mark.parametrize("group", [None, "32", "4096"])
+def test_batch_4096_corrupted_quad_fchain(ctx, monkeypatch, group):
     """the same 41-in-4,096 batch with the four-proofs-per-lane f-chain forced (ZG_FCHAIN_QUADS=1,
     split launches): the quad tree level has no pair nodes below it, and bisection must still
-    reach the exact reject set; GT of the clean batch equals the pair path's"""
+    reach the exact reject set. group: ZG_LINE_GROUP -- default (below 65,536 proofs the quad chain),
+    32 (group line products of 32 proofs: no tree below the groups until bisection runs the quad
+    chain), 4096 (one group: the chain writes the root)"""
     from zebra_amd import Context
     proofs, kinds, inputs, want = corrupted_4096(ctx)
     monkeypatch.setenv("ZG_FCHAIN_QUADS", "1")
     monkeypatch.setenv("ZG_LINES_FCHAIN", "0")
+    if group is not None:
+        monkeypatch.setenv("ZG_LINE_GROUP", group)
     q = Context(device=0, max_batch=4096)
     try:
         sts, _ = q.verify_batch(proofs, kinds, inputs)
@@ -149,6 +154,7 @@ def test_batch_4096_corrupted_quad_fchain(ctx, monkeypatch):
         q.close()
     assert sts == want
     assert st["quad_fchain_launches"] >= 1 and st["fused_launches"] == 0 and st["bisections"] == 1
+    assert st["line_product_batches"] == (0 if group is None else st["quad_fchain_launches"])
 
 
 def corrupted_4096(ctx):

@@ -42,8 +42,9 @@ def test_prog_schedule_structure():
             assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
             # B and C (outputs 4, 5) leave through their products' waves: no slot
             assert sorted(sch["sinks"].values()) == [4, 5], name
-        elif name in ("q4sq", "q4"):
-            # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse
+        elif name in ("q4sq", "q4", "gm", "gmsq"):
+            # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse (and the
+            # group chain's general products run in the same LDS budget, k_batch_fchaing)
             assert sch["nslots"] <= 25 and sch["rb"] == 1, name
         else:
             # no read barrier: a slot is never written in the round that reads its previous content
@@ -88,6 +89,12 @@ def test_fchain_programs():
         flat = [x for l in ls for x in l]
         assert run("q4", f12_pairs(f) + flat) == f12_pairs(f4)
         assert run("q4sq", f12_pairs(f) + flat) == f12_pairs(B.f12_sqr(f4))
+        # the group chain (k_batch_fchaing): f * L and (f * L)^2 for a general Fq12 L (the product
+        # of a group's lines at one step, k_line_prod)
+        g = B.f12_from_coeffs([rng.randrange(P) for _ in range(12)])
+        assert run("gm", f12_pairs(f) + f12_pairs(g)) == f12_pairs(B.f12_mul(f, g))
+        assert run("gmsq", f12_pairs(f) + f12_pairs(g)) == f12_pairs(B.f12_sqr(B.f12_mul(f, g)))
+
 
 
 def test_coop_tables():

@@ -50,6 +50,13 @@ for s in $STEPS; do
       env $envs timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs 8192 --steps 40 > $O/b8k_$cfg.json 2> $O/b8k_$cfg.err || { echo "bench 8k $cfg failed"; tail -20 $O/b8k_$cfg.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/b8k_$cfg.json')); print('8k $cfg', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s')"
     done ;;
+  envab)
+    # A/B of knobs over shard sizes, back to back: ENVS as env8k, SHARDS="65536 8192"
+    for n in ${SHARDS:-65536 8192}; do for cfg in default ${ENVS:-}; do
+      envs=""; [ "$cfg" != default ] && envs=$(echo $cfg | tr ',' ' ')
+      env $envs timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs $n --steps 40 > $O/ab_${n}_$cfg.json 2> $O/ab_${n}_$cfg.err || { echo "bench ab $n $cfg failed"; tail -20 $O/ab_${n}_$cfg.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/ab_${n}_$cfg.json')); print('$cfg shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s', {k: round(v,3) for k,v in d.get('phase_ms', {}).items()})"
+    done; done ;;
   inflight8k)
     # 8k shards at several batches-in-flight depths
     for inf in ${DEPTHS:-4 6 8 10}; do

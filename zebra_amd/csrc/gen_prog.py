@@ -252,6 +252,32 @@ def prog_q4():
     return p, f
 
 
+def f12_mul(p, a, b):
+    """pairing Fq12::mul (Karatsuba over Fq6): 18 products"""
+    aa = f6_mul(p, a[0:3], b[0:3])
+    bb = f6_mul(p, a[3:6], b[3:6])
+    s = f6_mul(p, [x + y for x, y in zip(a[0:3], a[3:6])], [x + y for x, y in zip(b[0:3], b[3:6])])
+    return [aa[i] + f6_nr(bb)[i] for i in range(3)] + [s[i] - aa[i] - bb[i] for i in range(3)]
+
+
+GEN_IN = ["F%d" % i for i in range(6)] + ["L%d" % i for i in range(6)]
+
+
+def prog_gm():
+    """f-chain step on a group's line product L_n (k_line_prod: the product over the group's proofs
+    of their step-n lines, a general Fq12) without the squaring: f = f * L. in: F0..F5 L0..L5."""
+    p = Prog("gm", GEN_IN)
+    ins = [p.inp(i) for i in range(12)]
+    return p, f12_mul(p, ins[0:6], ins[6:12])
+
+
+def prog_gmsq():
+    """the group f-chain step: f = (f * L)^2 (30 products for a whole group of proofs)."""
+    p = Prog("gmsq", GEN_IN)
+    ins = [p.inp(i) for i in range(12)]
+    return p, f12_sqr(p, f12_mul(p, ins[0:6], ins[6:12]))
+
+
 # ---------------------------------------------------------------- scheduling + slots
 # Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
 # Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
@@ -817,8 +843,9 @@ def emit(specs):
     prod_cases, out_cases = [], []
     infos, sched = [], []
     gk, go = 0, 0
-    for name, prog, outs, nw, sch in specs:
+    for pidx, (name, prog, outs, nw, sch) in enumerate(specs):
         nin = len(prog.inputs)
+        use = "if constexpr (M & (1u << %d))" % pidx  # the kernel's program mask (prog_run<RB, M>)
         # products
         for i, (L, R, kind) in enumerate(prog.prods):
             s = sch["slot"]
@@ -826,8 +853,8 @@ def emit(specs):
                 d = s[("p", i)]
                 dst = SINK_BASE + d[1] if isinstance(d, tuple) else d
                 lines, code = lazy_product(L, R, kind, s)
-                prod_cases.append("  case %d: {  // %s p%d round %d%s\n    %s\n    dst = %d; return %s;\n  }" % (
-                    gk + i, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else "",
+                prod_cases.append("  case %d: %s {  // %s p%d round %d%s\n    %s\n    dst = %d; return %s;\n  } break;" % (
+                    gk + i, use, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else "",
                     "\n    ".join(lines), dst, code))
                 continue
             if kind == K_SQR:
@@ -843,19 +870,19 @@ def emit(specs):
                     x, y = form_code(R, s, True), form_code(L, s, False)
             d = s[("p", i)]
             dst = SINK_BASE + d[1] if isinstance(d, tuple) else d
-            prod_cases.append("  case %d: x = %s; y = %s; dst = %d; return %d;  // %s p%d round %d%s" % (
-                gk + i, x, y, dst, kind, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else ""))
+            prod_cases.append("  case %d: %s { x = %s; y = %s; dst = %d; return %d; } break;  // %s p%d round %d%s" % (
+                gk + i, use, x, y, dst, kind, name, i, sch["rnd"][i], " -> HBM output %d" % d[1] if isinstance(d, tuple) else ""))
         for j, f in enumerate(outs):
             if j in sch.get("sinks", {}).values():
                 out_cases.append("  case %d: return f2_zero();  // %s out %d: stored by its product" % (go + j, name, j))
             elif LAZY:
                 lines, _ = lazy_form(f, sch["slot"], "v", True)
                 lines = hoist_loads(lines)
-                out_cases.append("  case %d: {  // %s out %d\n    Fq2 v;\n    %s\n    return v;\n  }" % (
-                    go + j, name, j, "\n    ".join(lines)))
+                out_cases.append("  case %d: %s {  // %s out %d\n    Fq2 v;\n    %s\n    return v;\n  } break;" % (
+                    go + j, use, name, j, "\n    ".join(lines)))
             else:
-                out_cases.append("  case %d: return %s;  // %s out %d" % (go + j, form_code(f, sch["slot"], False),
-                                                                        name, j))
+                out_cases.append("  case %d: %s { return %s; } break;  // %s out %d" % (
+                    go + j, use, form_code(f, sch["slot"], False), name, j))
         off = len(sched)
         for pick in sch["rounds"]:
             sched.extend([-1 if i is None else i for i in pick] + [-1] * (nw - len(pick)))
@@ -878,20 +905,30 @@ def emit(specs):
     out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
                sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
-    out.append("// operands of global product gk; returns the product kind (f2_mul_kind)")
+    out.append("// program mask of a kernel: ZG_PMASK(A) | ZG_PMASK(B) ... (bit k: program ZG_PROG_* = k)")
+    out.append("#define ZG_PMASK(P) (1u << ZG_PROG_##P)")
+    out.append("// operands of global product gk; returns the product kind (f2_mul_kind). M: the programs the")
+    out.append("// calling kernel runs -- only their cases are compiled in, so the register allocation of one")
+    out.append("// kernel does not carry the operand forms of every other program")
+    out.append("template <uint32_t M>")
     out.append("__device__ __forceinline__ int prog_operands(int gk, const AtomSpace& at, Fq2& x, Fq2& y, int& dst) {")
     out.append("  switch (gk) {")
     out.extend(prod_cases)
-    out.append("  default: x = y = f2_zero(); dst = 0; return 0;")
+    out.append("  default: break;")
     out.append("  }")
+    out.append("  x = y = f2_zero();")
+    out.append("  dst = 0;")
+    out.append("  return 0;")
     out.append("}")
+    out.append("template <uint32_t M>")
     out.append("__device__ __forceinline__ Fq2 prog_output(int go, const AtomSpace& at) {")
     out.append("  switch (go) {")
     out.extend(out_cases)
-    out.append("  default: return f2_zero();")
+    out.append("  default: break;")
     out.append("  }")
+    out.append("  return f2_zero();")
     out.append("}")
     out.append("}  // namespace zg")
     return out
@@ -904,7 +941,7 @@ LINES_MAX_SLOTS = 13
 
 
 SCHED_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zg_prog_sched.json")
-SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "dbl": 6000, "add": 6000}
+SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "dbl": 6000, "add": 6000}
 
 
 def build_all(search=None):
@@ -915,11 +952,13 @@ def build_all(search=None):
         cache = json.load(open(SCHED_CACHE))
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
-                   (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN)):
+                   (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN),
+                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
                                        prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
+                                       prog_gm: (0, True, True, 25), prog_gmsq: (0, True, True, 25),
                                        prog_dbl: (0, True, True, LINES_MAX_SLOTS),
                                        prog_add: (0, True, True, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
         share = 1 if fn in (prog_dbl, prog_add) else 2

@@ -35,8 +35,9 @@ using namespace zg;
 #define ZG_PIN_ENTRIES 584
 #define ZG_PIN_STATUS 640
 #define ZG_NTIMINGS 9
-#define ZG_NSTATS 11
+#define ZG_NSTATS 12
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
+#define ZG_LINE_PROD_MIN 65536   // shards from this many padded proofs run the f-chain as group line products
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
 #define ZG_K4_MIN 16384          // lone batches from this many (padded) proofs sum r_i C_i by K4's Pippenger
                                  // buckets; smaller lone batches by the GLV products in decode + the C tree
@@ -135,6 +136,7 @@ struct zg_ctx {
   G2A* d_ptB = nullptr;
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
+  Fq2* d_lprod = nullptr;  // cap / 4 x 68 x 6: per-group line products (k_line_prod)
   G1J* d_ctree = nullptr;
   Fr* d_stree = nullptr;
   MsmBufs msm = {};       // K4: Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)
@@ -164,6 +166,9 @@ struct zg_ctx {
                             // 2; the staged program below), 1 / 2 always straight-line sized for 2 / 1
                             // waves per SIMD, 0 always the staged program (zg_kernels.h)
   int quads = -1;            // ZG_FCHAIN_QUADS: -1 auto (npad >= ZG_QUAD_MIN), 0 never, 1 always (npad >= 4)
+  int line_group = -1;       // ZG_LINE_GROUP: proofs per group (k_line_prod): -1 auto (32 from ZG_LINE_PROD_MIN
+                             // padded proofs, else the quad chain), 0 never, a power of two >= 4 always
+  int lineprod_last = 0;     // the last batch's f-chain ran on group line products (no tree below the groups)
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
@@ -301,6 +306,8 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_LINES_FCHAIN")) ctx->fuse = atoi(e);
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
+  if (const char* e = getenv("ZG_LINE_GROUP")) ctx->line_group = atoi(e);
+  if (ctx->line_group != -1 && (ctx->line_group < 4 || (ctx->line_group & (ctx->line_group - 1)))) ctx->line_group = 0;
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_FCHAIN_SINGLE")) ctx->singles = atoi(e);
   if (const char* e = getenv("ZG_LINES_LANE")) ctx->lines_lane = atoi(e);
@@ -326,6 +333,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_ptB, cap));
   A(dalloc(&ctx->d_ftree, 2 * (size_t)cap));
   A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
+  if (ctx->line_group) A(dalloc(&ctx->d_lprod, ((size_t)cap / 4 + 1) * ZG_NCOEFF * 6));
   A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
   A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT_MAX));
@@ -370,7 +378,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   if (ctx->bn_key && ctx->dev) zg::bn_key_release(ctx->dev->bn, ctx->bn_key);
   void* ptrs[] = {ctx->d_vk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
-                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines,
+                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines, ctx->d_lprod,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
                   ctx->msm.entries, ctx->msm.cd, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
                   ctx->bn_arena, ctx->d_dbg};
@@ -721,6 +729,8 @@ hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchB
                                    const int* nodes, int m);
 hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
 hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines);
+hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize);
+hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, int m);
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
                                     int* fail, int per);
 hipError_t launch_prog_fchain1(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
@@ -747,6 +757,18 @@ static hipError_t launch_c_tree(zg_ctx* ctx, const BatchBufs& b, hipStream_t st,
   for (size_t lo = ctx->npad / 2; lo >= 1; lo /= 2)
     hipLaunchKernelGGL(k_tree_c, dim3(nblocks(lo * ZG_NKINDS)), dim3(ZG_BLOCK), 0, st, b, (int)lo, gate);
   return hipGetLastError();
+}
+// the Fq12 product-tree levels above `top` nodes (ftree[top .. 2 top) written), root ftree[1]
+static hipError_t launch_f_tree(zg_ctx* ctx, const BatchBufs& b, size_t top) {
+  for (size_t lo = top / 2; lo >= 1; lo /= 2) {
+    if (lo >= ctx->coop_below)
+      hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
+    else
+      hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
@@ -806,6 +828,14 @@ static int run_pipeline(zg_ctx* ctx) {
   // per four proofs and step instead of 76 (k_batch_fchain4)
   const bool quads = !fused && ctx->npad >= 4 && (ctx->quads == 1 || (ctx->quads < 0 && ctx->npad >= ZG_QUAD_MIN));
   ctx->quads_last = quads;
+  // group line products (k_line_prod + k_batch_fchaing) instead of the quad chain: auto from
+  // ZG_LINE_PROD_MIN, 32 proofs a group (in flight, ms per batch, quad chain -> groups of 16 / 32 / 64:
+  // 64k 13.67 -> 12.97 / 12.75 / 12.90, 32k 7.26 -> 7.24 at 32 and 64, 16k 4.17 -> 4.38 at 32, 8k 2.63 -> 2.89
+  // at 32; profiles/r05p_lineprod_ab.txt)
+  int gsize = ctx->line_group < 0 ? (ctx->npad >= ZG_LINE_PROD_MIN ? 32 : 0) : ctx->line_group;
+  if ((size_t)gsize > ctx->npad) gsize = 0;
+  const bool lineprod = quads && gsize;
+  ctx->lineprod_last = lineprod;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
@@ -831,20 +861,19 @@ static int run_pipeline(zg_ctx* ctx) {
       HIPCHK(launch_prog_lines(groups, ctx->stream, b, ctx->d_lines));
     }
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
-    if (quads)
-      HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines));
-    else
+    const unsigned qgroups = (unsigned)((ctx->npad / 4 + 63) / 64);
+    if (lineprod) {  // group line products, one chain per group (k_line_prod, k_batch_fchaing)
+      HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize));
+      HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, (int)(ctx->npad / gsize)));
+    } else if (quads) {
+      HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines));
+    } else {
       HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)nullptr));
+    }
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  for (size_t lo = ctx->npad / (singles ? 2 : quads ? 8 : 4); lo >= 1; lo /= 2) {
-    if (lo >= ctx->coop_below)
-      hipLaunchKernelGGL(k_tree_f, dim3(nblocks(lo)), dim3(ZG_BLOCK), 0, ctx->stream, b, (int)lo);
-    else
-      hipLaunchKernelGGL(k_tree_f_coop, dim3((unsigned)lo), dim3(64), 0, ctx->stream, b, (int)lo);
-    HIPCHK(hipGetLastError());
-  }
+  HIPCHK(launch_f_tree(ctx, b, lineprod ? ctx->npad / gsize : ctx->npad / (singles ? 1 : quads ? 4 : 2)));
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   if (ctx->serial_side) {
     if ((rc = side_work(ctx->stream))) return rc;
@@ -1025,6 +1054,7 @@ static int collect_batch_stats(zg_ctx* ctx) {
   ctx->stats[0]++;
   if (ctx->fused_last) ctx->stats[1]++;
   if (ctx->quads_last) ctx->stats[7]++;
+  if (ctx->lineprod_last) ctx->stats[11]++;
   if (flags[1]) {
     ctx->stats[2]++;
     ctx->fuse_off = 1;
@@ -1132,6 +1162,13 @@ extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
 static int build_trees(zg_ctx* ctx) {
   if (ctx->trees_built) return ZG_OK;
   BatchBufs b = batch_bufs(ctx);
+  // group line products: the tree exists from the groups up only; the quad f-chain on the lines
+  // (still in HBM) and the levels above write every node (those from the groups up again, with
+  // the same values)
+  if (ctx->lineprod_last) {
+    HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines));
+    HIPCHK(launch_f_tree(ctx, b, ctx->npad / 4));
+  }
   HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));
   HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[10], 0));
   // small shards (k4_last = 0): the pipeline already built the whole C tree from the GLV leaves

@@ -27,6 +27,13 @@ namespace zg {
 #define ZG_FC_NW 8      // 2 waves per SIMD (256 VGPRs, no spills); msq = 4 rounds
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
 #define ZG_PUB_STEPS 4  // fused launch: lines steps per publish
+// operand-switch masks of prog_run (zg_prog.h): the programs DBL .. Q4 of round 4 (their kernels'
+// register allocation as measured then); for k_line_prod (Q4 only) the switch through GM: a
+// search over supersets of Q4 gives 40 B/lane of scratch for DBL .. GM against 72 for all
+// programs and 136 for DBL .. Q4 or Q4 alone (tools/resource_table.py, guarded by
+// tests/test_resources.py)
+#define ZG_PMASK_R4 0xffu
+#define ZG_LP_MASK 0x1ffu
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
   return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
@@ -73,9 +80,9 @@ __device__ __forceinline__ void lines_body(const BatchBufs& b, Fq2* lines, int b
       if (pass == 1 && (i < 0 || !((ZG_XH >> i) & 1ull))) break;
       const int pid = pass == 0 ? ZG_PROG_DBL : ZG_PROG_ADD;
       Fq2* sink = proof < b.npad ? lines + ((size_t)n * b.npad + proof) * 3 : nullptr;
-      prog_run<true>(pid, atq, sink, act);
+      prog_run<true, ZG_PMASK_R4>(pid, atq, sink, act);
       Fq2 v;
-      if (wave < 4) v = prog_output(PROG_INFO[pid].go + wave, atq);
+      if (wave < 4) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, atq);
       __syncthreads();
       if (wave < 3)
         at.put(wave, v);
@@ -178,9 +185,9 @@ __device__ __forceinline__ void fchain_body(const BatchBufs& b, const Fq2* lines
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_MM : ZG_PROG_MMSQ);
-      prog_run<false>(pid, at);
+      prog_run<false, ZG_PMASK_R4>(pid, at);
       Fq2 v;
-      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      if (wave < 6) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, at);
       __syncthreads();
       n++;
       if (wave < 6)
@@ -244,9 +251,9 @@ __device__ __forceinline__ void fchain1_body(const BatchBufs& b, const Fq2* line
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
-      prog_run<false>(pid, at);
+      prog_run<false, ZG_PMASK_R4>(pid, at);
       Fq2 v;
-      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      if (wave < 6) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, at);
       __syncthreads();
       n++;
       if (wave < 6)
@@ -310,10 +317,10 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_Q4 : ZG_PROG_Q4SQ);
       ZG_TRACE_S(n, 0);
-      prog_run<true>(pid, at);
+      prog_run<true, ZG_PMASK_R4>(pid, at);
       ZG_TRACE_S(n, 1);
       Fq2 v;
-      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      if (wave < 6) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, at);
       ZG_TRACE_S(n, 2);
       __syncthreads();
       ZG_TRACE_S(n, 3);
@@ -333,6 +340,90 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     reinterpret_cast<Fq2*>(&b.ftree[b.npad / 4 + quad])[wave] = v;
   }
 }
+// Group line products (large shards): the Miller values of a group's proofs multiply into one
+// node, and every Miller loop squares at the same steps, so the group's value is ONE Miller chain
+// over the products L_n = prod_i l_{i,n} of the group's step-n lines:
+//   prod_i f_i = chain_n (f <- (f L_n)^2 or f L_n).
+// The L_n of all steps are independent of each other: k_line_prod forms them at full occupancy
+// (lane = (step, group), Q4 programs f <- f l_4t l_4t+1 l_4t+2 l_4t+3 over the group's lines, 13
+// products per proof and step, no squaring) and the sequential part shrinks to one chain per
+// group (k_batch_fchaing, GMSQ: 30 products per step for the whole group). Against the quad
+// chain (Q4SQ, 16 products per proof-step, all on the 68-step sequential path) that is 13 + 30 / G.
+// lprod layout: [n][6][m] (m = npad / G groups; coefficient-major, coalesced on lane = group).
+__device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int blk,
+                                              const AtomSpace& at) {
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const size_t m = (size_t)b.npad / gsize;
+  const int bps = (int)((m + 63) / 64);
+  const int n = blk / bps;
+  const size_t g = (size_t)(blk % bps) * 64 + lane;
+  const bool inb = g < m;
+  const int p0 = inb ? (int)(g * gsize) : 0;
+  const Fq2* src0 = lines + ((size_t)n * b.npad + p0) * 3;
+  // the lines of proofs p0 + 4t .. p0 + 4t + 3 into slots 6..17 (atom j by wave (j + 6) mod 8)
+  auto load = [&](int t) {
+    for (int j = (wave + 2) & 7; j < 12; j += 8) {
+      const bool act = inb && proof_active(b, p0 + 4 * t + j / 3);
+      at.put(6 + j, act ? src0[12 * t + j] : (j % 3 == 0 ? f2_one() : f2_zero()));
+    }
+  };
+  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  for (int t = 0; t < gsize / 4; t++) {
+    load(t);
+    __syncthreads();
+    prog_run<true, ZG_LP_MASK>(ZG_PROG_Q4, at);
+    Fq2 v;
+    if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[ZG_PROG_Q4].go + wave, at);
+    __syncthreads();
+    if (wave < 6) at.put(wave, v);
+  }
+  if (wave < 6 && inb) lprod[((size_t)n * 6 + wave) * m + g] = at.get(wave);
+}
+// one Miller chain per group over its line products; writes the tree level of groups (m nodes)
+__device__ __forceinline__ void fchaing_body(const BatchBufs& b, const Fq2* lprod, int m, int blk, const AtomSpace& at) {
+  const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
+  const int g = blk * 64 + lane;
+  const bool inb = g < m;
+  auto load_l = [&](int n) {
+    const int s = (wave + 2) & 7;
+    if (s < 6) at.put(6 + s, lprod[((size_t)n * 6 + s) * m + (inb ? g : 0)]);
+  };
+  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  load_l(0);
+  __syncthreads();
+  int n = 0;
+  for (int i = ZG_XH_TOP;; i--) {
+    const bool last = i < 0;
+    const bool addbit = !last && ((ZG_XH >> i) & 1ull);
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_GM : ZG_PROG_GMSQ);
+      prog_run<true, ZG_PMASK(GM) | ZG_PMASK(GMSQ)>(pid, at);
+      Fq2 v;
+      if (wave < 6) v = prog_output<ZG_PMASK(GM) | ZG_PMASK(GMSQ)>(PROG_INFO[pid].go + wave, at);
+      __syncthreads();
+      n++;
+      if (wave < 6) at.put(wave, v);
+      if (n < ZG_NCOEFF) load_l(n);
+      __syncthreads();
+    }
+    if (last) break;
+  }
+  if (wave < 6 && inb) {
+    Fq2 v = at.get(wave);
+    if (wave >= 3) v = f2_neg(v);  // conjugate (u < 0)
+    reinterpret_cast<Fq2*>(&b.ftree[m + g])[wave] = v;
+  }
+}
+#if defined(ZG_TU_PROG_FCHAIN4)
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_line_prod(BatchBufs b, const Fq2* lines, Fq2* lprod, int gsize) {
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  lineprod_body(b, lines, lprod, gsize, blockIdx.x, AtomSpace{lds_atoms});
+}
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, const Fq2* lprod, int m) {
+  __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
+  fchaing_body(b, lprod, m, blockIdx.x, AtomSpace{lds_atoms});
+}
+#endif
 #if defined(ZG_TU_PROG_FCHAIN4)
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, const Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
@@ -393,9 +484,9 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_leaf_fchain(BatchBufs b, cons
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_M : ZG_PROG_MSQ);
-      prog_run<false>(pid, at);
+      prog_run<false, ZG_PMASK_R4>(pid, at);
       Fq2 v;
-      if (wave < 6) v = prog_output(PROG_INFO[pid].go + wave, at);
+      if (wave < 6) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, at);
       __syncthreads();
       n++;
       if (wave < 6)
