@@ -116,13 +116,17 @@ def _ctx_env(env, n):
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 4},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 2048},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32},
+                                 {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_LINE_PROD_PARTS": 1},
+                                 {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_LINE_PROD_PARTS": 3},
+                                 {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_SERIAL_SIDE": 1},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_LINES_LANE": 1}, {"ZG_K4_MIN": 1}],
                          ids=lambda e: ",".join("%s=%s" % kv for kv in e.items()))
 def test_context_knobs_give_the_same_partial(work4k, env):
     """every per-context schedule switch (zg.hip zg_create: side work serialised on the main stream,
     product-tree levels lane-per-node or wave-per-node, the fused launch with proof pairs instead of
     single proofs, split quads as group line products + per-group chains (4, 32 or all 2,048
-    proofs a group) or as the quad chain, the straight-line R-chain, K4 on a lone small batch) computes the
+    proofs a group; their chains in 1, 3 or 4 step parts overlapping the line products) or as the quad
+    chain, the straight-line R-chain, K4 on a lone small batch) computes the
     same batch: byte-identical 576-B Miller partial to the default schedule's for seeded scalars"""
     n = 2048
     proofs, kinds, inputs = work4k

@@ -42,7 +42,7 @@ def test_prog_schedule_structure():
             assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
             # B and C (outputs 4, 5) leave through their products' waves: no slot
             assert sorted(sch["sinks"].values()) == [4, 5], name
-        elif name in ("q4sq", "q4", "gm", "gmsq"):
+        elif name in ("q4sq", "q4", "gm", "gmsq", "q4i"):
             # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse (and the
             # group chain's general products run in the same LDS budget, k_batch_fchaing)
             assert sch["nslots"] <= 25 and sch["rb"] == 1, name
@@ -88,6 +88,12 @@ def test_fchain_programs():
             f4 = B.f12_mul(f4, ((a_, b_, B.F2_ZERO), (B.F2_ZERO, c_, B.F2_ZERO)))
         flat = [x for l in ls for x in l]
         assert run("q4", f12_pairs(f) + flat) == f12_pairs(f4)
+        # a group's first four lines from scratch (k_line_prod): (l0 l1)(l2 l3), f unused
+        assert run("q4i", f12_pairs(f) + flat) == f12_pairs(B.f12_mul(B.f12_mul(B.f12_mul(
+            ((ls[0][0], ls[0][1], B.F2_ZERO), (B.F2_ZERO, ls[0][2], B.F2_ZERO)),
+            ((ls[1][0], ls[1][1], B.F2_ZERO), (B.F2_ZERO, ls[1][2], B.F2_ZERO))),
+            ((ls[2][0], ls[2][1], B.F2_ZERO), (B.F2_ZERO, ls[2][2], B.F2_ZERO))),
+            ((ls[3][0], ls[3][1], B.F2_ZERO), (B.F2_ZERO, ls[3][2], B.F2_ZERO))))
         assert run("q4sq", f12_pairs(f) + flat) == f12_pairs(B.f12_sqr(f4))
         # the group chain (k_batch_fchaing): f * L and (f * L)^2 for a general Fq12 L (the product
         # of a group's lines at one step, k_line_prod)

@@ -52,9 +52,9 @@ def test_fchain4_fits_one_block_per_cu(kernels):
 
 
 def test_group_line_product_kernels_fit(kernels):
-    """k_line_prod / k_batch_fchaing: one block per CU, two waves per SIMD, at most 64 B/lane of
+    """k_line_prod / k_batch_fchaing: one block per CU, two waves per SIMD, at most 32 B/lane of
     scratch (their program masks are chosen for that, zg_prog.h prog_run)"""
     for part in ("k_line_prod", "k_batch_fchaing"):
         (name, r), = _find(kernels, part).items()
-        assert r["lds"] <= 160 * 1024 and r["vgpr"] <= 256 and r["occ"] >= 2 and r["scratch"] <= 64, (name, r)
+        assert r["lds"] <= 160 * 1024 and r["vgpr"] <= 256 and r["occ"] >= 2 and r["scratch"] <= 32, (name, r)
 

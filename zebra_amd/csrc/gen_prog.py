@@ -278,6 +278,36 @@ def prog_gmsq():
     return p, f12_sqr(p, f12_mul(p, ins[0:6], ins[6:12]))
 
 
+def line_pair(p, l, l2):
+    """the product of two sparse lines (A + B v) + (C v) w as (E0 + E1 v + E2 v^2) + (E4 v + E5 v^2) w
+    (w^2 = v, v^3 = xi): 6 products"""
+    A, B, C = l
+    A2, B2, C2 = l2
+    aa, bb, cc = p.mul(A, A2), p.mul(B, B2), p.mul(C, C2)
+    return [aa + cc.nr(), p.mul(A + B, A2 + B2) - aa - bb, bb, p.mul(A + C, A2 + C2) - aa - cc,
+            p.mul(B + C, B2 + C2) - bb - cc]
+
+
+def pair_pair(p, P, P2):
+    """the product of two line pairs (c1[0] = 0 in both): 15 products, a general Fq12"""
+    E0, E1, E2, E4, E5 = P
+    F0, F1, F2, F4, F5 = P2
+    aa = f6_mul(p, [E0, E1, E2], [F0, F1, F2])
+    xx, yy = p.mul(E4, F4), p.mul(E5, F5)
+    bb = [(p.mul(E4 + E5, F4 + F5) - xx - yy).nr(), yy.nr(), xx]  # (x v + y v^2)(x' v + y' v^2)
+    s = f6_mul(p, [E0, E1 + E4, E2 + E5], [F0, F1 + F4, F2 + F5])
+    return [aa[i] + f6_nr(bb)[i] for i in range(3)] + [s[i] - aa[i] - bb[i] for i in range(3)]
+
+
+def prog_q4i():
+    """a group's first four lines (k_line_prod): l_0 l_1 l_2 l_3 from scratch as (l_0 l_1)(l_2 l_3),
+    27 products (Q4 on f = 1: 52). in: F0..F5 (unused), then A B C of the four proofs."""
+    p = Prog("q4i", ["F%d" % i for i in range(6)] + ["%s%d" % (c, j) for j in range(4) for c in "ABC"])
+    ins = [p.inp(i) for i in range(18)]
+    ls = [ins[6 + 3 * j: 9 + 3 * j] for j in range(4)]
+    return p, pair_pair(p, line_pair(p, ls[0], ls[1]), line_pair(p, ls[2], ls[3]))
+
+
 # ---------------------------------------------------------------- scheduling + slots
 # Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
 # Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
@@ -905,7 +935,7 @@ def emit(specs):
     out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
                sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq", "q4i")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
     out.append("// program mask of a kernel: ZG_PMASK(A) | ZG_PMASK(B) ... (bit k: program ZG_PROG_* = k)")
     out.append("#define ZG_PMASK(P) (1u << ZG_PROG_##P)")
@@ -941,7 +971,7 @@ LINES_MAX_SLOTS = 13
 
 
 SCHED_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zg_prog_sched.json")
-SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "dbl": 6000, "add": 6000}
+SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "q4i": 3000, "dbl": 6000, "add": 6000}
 
 
 def build_all(search=None):
@@ -953,12 +983,13 @@ def build_all(search=None):
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
                    (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN),
-                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN)):
+                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN), (prog_q4i, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
                                        prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
                                        prog_gm: (0, True, True, 25), prog_gmsq: (0, True, True, 25),
+                                       prog_q4i: (0, True, True, 25),
                                        prog_dbl: (0, True, True, LINES_MAX_SLOTS),
                                        prog_add: (0, True, True, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
         share = 1 if fn in (prog_dbl, prog_add) else 2

@@ -28,7 +28,8 @@ using namespace zg;
 
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
-#define ZG_NEV 14  // [13]: zg_gt_check
+#define ZG_NEV 19  // [13]: zg_gt_check; [14..17] line-product parts, [18] their chains done (no timing)
+#define ZG_LP_PARTS_MAX 4
 // the pinned host block of a context: the root's 576-B Miller partial, the pipeline flags
 // (bfail, fused-wait failure), the K4 entry count, then the n statuses
 #define ZG_PIN_FLAGS 576
@@ -137,6 +138,7 @@ struct zg_ctx {
   Fq12* d_ftree = nullptr;
   Fq2* d_lines = nullptr;  // cap x 68 x 3: per-proof line triples (R-chain -> f-chain)
   Fq2* d_lprod = nullptr;  // cap / 4 x 68 x 6: per-group line products (k_line_prod)
+  Fq2* d_fstate = nullptr; // cap / 4 x 6: each group chain's f between its parts (k_batch_fchaing)
   G1J* d_ctree = nullptr;
   Fr* d_stree = nullptr;
   MsmBufs msm = {};       // K4: Pippenger sum r_i C_i per key + root Fr sums (zg_msm.h)
@@ -156,6 +158,8 @@ struct zg_ctx {
   // them), or the caller's HBM-resident buffers (zg_batch_begin_device: read in place, no copy)
   const uint8_t *cur_proofs = nullptr, *cur_kinds = nullptr, *cur_inputs = nullptr;
   int root_pairs_ready = 0;  // the pipeline already ran the root's MSM + VK pairs on `side`
+  int settled = 0;           // settle_batch ran for this batch
+  int alone_last = 0;        // the last batch ran with no other batch in flight (K4 shape)
   int eager = 0;             // the pipeline's last steps copied the root partial, flags and statuses to h_pin (ev[4])
   uint8_t* h_pin = nullptr;  // pinned host memory: ZG_PIN_* layout
   uint8_t* h_gt = nullptr;   // pinned staging of zg_gt_check (partials in, verdict out; grow-only)
@@ -169,6 +173,7 @@ struct zg_ctx {
   int line_group = -1;       // ZG_LINE_GROUP: proofs per group (k_line_prod): -1 auto (32 from ZG_LINE_PROD_MIN
                              // padded proofs, else the quad chain), 0 never, a power of two >= 4 always
   int lineprod_last = 0;     // the last batch's f-chain ran on group line products (no tree below the groups)
+  int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..4)
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
@@ -307,6 +312,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_LINE_GROUP")) ctx->line_group = atoi(e);
+  if (const char* e = getenv("ZG_LINE_PROD_PARTS")) ctx->lp_parts = std::max(1, std::min(ZG_LP_PARTS_MAX, atoi(e)));
   if (ctx->line_group != -1 && (ctx->line_group < 4 || (ctx->line_group & (ctx->line_group - 1)))) ctx->line_group = 0;
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_FCHAIN_SINGLE")) ctx->singles = atoi(e);
@@ -334,6 +340,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_ftree, 2 * (size_t)cap));
   A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
   if (ctx->line_group) A(dalloc(&ctx->d_lprod, ((size_t)cap / 4 + 1) * ZG_NCOEFF * 6));
+  if (ctx->line_group) A(dalloc(&ctx->d_fstate, ((size_t)cap / 4 + 1) * 6));
   A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
   A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT_MAX));
@@ -351,7 +358,8 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_out, ZG_NODE_CHUNK));
   if (ctx->debug_each) A(dalloc(&ctx->d_dbg, cap));
   A(hipHostMalloc((void**)&ctx->h_pin, ZG_PIN_STATUS + (size_t)cap, hipHostMallocDefault));
-  for (int i = 0; i < ZG_NEV; i++) A(hipEventCreate(&ctx->ev[i]));
+  for (int i = 0; i < ZG_NEV; i++)
+    A(i < 14 ? hipEventCreate(&ctx->ev[i]) : hipEventCreateWithFlags(&ctx->ev[i], hipEventDisableTiming));
   // surface a broken device / stream now rather than inside a later batch
   A(hipMemsetAsync(ctx->d_vk, 0, sizeof(DevVK) * ZG_NKINDS, ctx->stream));
   A(hipMemsetAsync(ctx->d_int, 0, sizeof(int) * 16, ctx->side));
@@ -378,7 +386,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
   if (ctx->bn_key && ctx->dev) zg::bn_key_release(ctx->dev->bn, ctx->bn_key);
   void* ptrs[] = {ctx->d_vk, ctx->d_int, ctx->d_proofs, ctx->d_kinds, ctx->d_inputs, ctx->d_ninputs,
                   ctx->d_r, ctx->d_status, ctx->d_bytes, ctx->d_ptA, ctx->d_ptB, ctx->d_ftree, ctx->d_ctree,
-                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines, ctx->d_lprod,
+                  ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines, ctx->d_lprod, ctx->d_fstate,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
                   ctx->msm.entries, ctx->msm.cd, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
                   ctx->bn_arena, ctx->d_dbg};
@@ -729,8 +737,10 @@ hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchB
                                    const int* nodes, int m);
 hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
 hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines);
-hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize);
-hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, int m);
+hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
+                                int n1);
+hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,
+                               int n1);
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
                                     int* fail, int per);
 hipError_t launch_prog_fchain1(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
@@ -773,8 +783,9 @@ static hipError_t launch_f_tree(zg_ctx* ctx, const BatchBufs& b, size_t top) {
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   ctx->eager = 0;
-  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ctx->d_nodes, 1, 1, ctx->stream));  // node list = {root}
-  HIPCHK(hipMemsetAsync(b.bfail, 0, 2 * sizeof(int), ctx->stream));  // bfail, fused-wait failure
+  // the flags (bfail, fused-wait failure) are cleared by the first kernel (k_decode_sqrt); the root's node
+  // list is implicit (NodeBufs::nodes null)
+  ctx->settled = 0;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   const unsigned dgroups = (unsigned)((ctx->npad + 63) / 64);
   // a lone small batch is latency-bound: the GLV products ride on decode and the tree replaces K4's
@@ -789,7 +800,8 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   ctx->trees_built = 0;
   ctx->c_tree_pending = 0;
-  NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
+  NodeBufs nb = {nullptr, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
+  ctx->alone_last = alone;
   // side stream: K4 + the root's VK-side work (or, serial_side, on the main stream after the tree)
   auto side_work = [&](hipStream_t st) -> int {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
@@ -863,8 +875,24 @@ static int run_pipeline(zg_ctx* ctx) {
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     const unsigned qgroups = (unsigned)((ctx->npad / 4 + 63) / 64);
     if (lineprod) {  // group line products, one chain per group (k_line_prod, k_batch_fchaing)
-      HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize));
-      HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, (int)(ctx->npad / gsize)));
+      // in parts of the 68 steps: the side stream (its K4 / VK work long done by then) runs the
+      // chains over part k while the main stream forms part k + 1, so the chains' latency hides
+      // behind the line products except for the last part
+      const int m = (int)(ctx->npad / gsize), parts = ctx->lp_parts;
+      if (parts <= 1) {
+        HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, 0, ZG_NCOEFF));
+        HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, 0, ZG_NCOEFF));
+      } else {
+        for (int k = 0; k < parts; k++) {
+          const int n0 = ZG_NCOEFF * k / parts, n1 = ZG_NCOEFF * (k + 1) / parts;
+          HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, n0, n1));
+          HIPCHK(hipEventRecord(ctx->ev[14 + k], ctx->stream));
+          HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[14 + k], 0));
+          HIPCHK(launch_prog_fchaing(ctx->side, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, n0, n1));
+        }
+        HIPCHK(hipEventRecord(ctx->ev[18], ctx->side));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[18], 0));
+      }
     } else if (quads) {
       HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines));
     } else {
@@ -880,11 +908,8 @@ static int run_pipeline(zg_ctx* ctx) {
   } else {
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream K4 + root pairs complete
   }
-  // deferred-B recompute (no-ops unless a B_i failed its subgroup check in k_batch_lines)
-  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, b.bfail, nullptr, nullptr, k4, alone));
-  if (!k4) HIPCHK(launch_c_tree(ctx, b, ctx->stream, b.bfail));
-  rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream, b.bfail);
-  if (rc) return rc;
+  // a B_i that failed its subgroup check in the R-chain (invalid proofs only) was still in the side
+  // stream's root sums: settle_batch recomputes them when the flags say so
   ctx->root_pairs_ready = 1;
   // the root's Miller partial, the pipeline flags and the statuses go to pinned host memory as the
   // last steps (ev[4]), so zg_batch_partial / zg_batch_finish find them ready: computed only when
@@ -1006,7 +1031,8 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
   const bool reuse_root = ctx->root_pairs_ready && nodes.size() == 1 && nodes[0] == 1;
   for (size_t off = 0; off < nodes.size(); off += ZG_NODE_CHUNK) {
     int m = (int)std::min((size_t)ZG_NODE_CHUNK, nodes.size() - off);
-    NodeBufs nb = {ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, m};
+    // the pipeline's root pairs: its node list is implicit (null: the root)
+    NodeBufs nb = {reuse_root ? nullptr : ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, m};
     if (!reuse_root) {
       ctx->root_pairs_ready = 0;  // d_msm / d_pairf are about to be overwritten
       HIPCHK(hipMemcpyAsync(ctx->d_nodes, nodes.data() + off, sizeof(int) * m, hipMemcpyHostToDevice, ctx->stream));
@@ -1075,13 +1101,41 @@ static int collect_batch_stats(zg_ctx* ctx) {
   return ZG_OK;
 }
 
+// After the pipeline's last step: if a B_i failed its G2 subgroup check in the R-chain (flags[0],
+// invalid proofs only), the side stream's root work -- K4 / the C tree, the root's VK-side MSM and
+// pairs -- ran with that proof still in; recompute it without (its leaves were cleared by the R-chain
+// kernel), then the root partial. A valid batch pays nothing here: round 4 queued this recompute as
+// ~12 gated no-op launches at the end of every batch's main stream.
+static int settle_batch(zg_ctx* ctx) {
+  HIPCHK(wait_event(ctx->ev[4]));
+  if (ctx->settled) return ZG_OK;
+  ctx->settled = 1;
+  int flags[2] = {0, 0};
+  memcpy(flags, ctx->h_pin + ZG_PIN_FLAGS, sizeof(flags));
+  if (!flags[0]) return ZG_OK;
+  BatchBufs b = batch_bufs(ctx);
+  NodeBufs nb = {nullptr, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
+  HIPCHK(launch_msm_root(ctx->stream, b, ctx->msm, nullptr, nullptr, nullptr, ctx->k4_last, ctx->alone_last));
+  if (!ctx->k4_last) HIPCHK(launch_c_tree(ctx, b, ctx->stream, nullptr));
+  int rc = launch_node_msm_pairs(ctx, b, nb, ctx->stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_node_partial, dim3(1), dim3(64), 0, ctx->stream, b, nb);
+  hipLaunchKernelGGL(k_f12_to_bytes, dim3(1), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_out, 1, ctx->d_bytes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->h_pin, ctx->d_bytes, 576, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  HIPCHK(wait_event(ctx->ev[4]));
+  return ZG_OK;
+}
+
 extern "C" int zg_batch_partial(zg_ctx* ctx, uint8_t partial[576]) {
   if (!ctx || !partial) return ZG_E_INVAL;
   std::lock_guard<std::mutex> g(ctx->mu);
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_partial before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
   if (!ctx->eager) return fail(ctx, ZG_E_STATE, "zg_batch_partial: no pipeline result");
-  HIPCHK(wait_event(ctx->ev[4]));
+  int rc = settle_batch(ctx);
+  if (rc) return rc;
   memcpy(partial, ctx->h_pin, 576);
   return collect_batch_stats(ctx);
 }
@@ -1252,8 +1306,11 @@ static int batch_finish_locked(zg_ctx* ctx, int batch_ok, uint8_t* status, bool 
   if (ctx->state != 1) return fail(ctx, ZG_E_STATE, "zg_batch_finish before zg_batch_begin");
   HIPCHK(hipSetDevice(ctx->device));
   std::vector<uint8_t> st(ctx->n);
+  if (ctx->eager) {
+    int rc = settle_batch(ctx);
+    if (rc) return rc;
+  }
   if (ctx->eager && batch_ok) {  // the pipeline's own status copy (run_pipeline, ev[4])
-    HIPCHK(wait_event(ctx->ev[4]));
     if (ctx->n) memcpy(st.data(), ctx->h_pin + ZG_PIN_STATUS, ctx->n);
   } else {
     if (ctx->n) HIPCHK(hipMemcpyAsync(st.data(), ctx->d_status, ctx->n, hipMemcpyDeviceToHost, ctx->stream));
@@ -1301,6 +1358,10 @@ extern "C" int zg_verify_batch(zg_ctx* ctx, size_t n, const uint8_t* proofs, con
   std::lock_guard<std::mutex> g(ctx->mu);
   int rc = batch_begin_locked(ctx, n, proofs, kinds, inputs, n_inputs, r);
   if (rc) return rc;
+  if ((rc = settle_batch(ctx))) {
+    set_state(ctx, 0);
+    return rc;
+  }
   std::vector<int> root = {1}, okv;
   if (gt_out) rc = check_nodes(ctx, root, 2, nullptr, gt_out);
   if (!rc) rc = check_nodes(ctx, root, 0, &okv, nullptr);

@@ -54,6 +54,9 @@ namespace zg {
 __global__ void __launch_bounds__(64, ZG_DECODE_SQRT_WPE) k_decode_sqrt(BatchBufs b) {
   const int role = blockIdx.x & 1;  // 0 A, 1 C (wave-uniform)
   const int i = (blockIdx.x >> 1) * 64 + (threadIdx.x & 63);
+  // the pipeline's first kernel clears the batch flags (B subgroup failures, fused-wait failure):
+  // no fill launch in front of the batch
+  if (blockIdx.x == 0 && threadIdx.x < 2) b.bfail[threadIdx.x] = 0;
   if (i >= b.npad) return;
   G1A p;
   p.inf = true;

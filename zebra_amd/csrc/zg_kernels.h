@@ -28,12 +28,11 @@ namespace zg {
 #define ZG_ATOM_BYTES (ZG_ATOM_ROWS * 64 * 16)
 #define ZG_PUB_STEPS 4  // fused launch: lines steps per publish
 // operand-switch masks of prog_run (zg_prog.h): the programs DBL .. Q4 of round 4 (their kernels'
-// register allocation as measured then); for k_line_prod (Q4 only) the switch through GM: a
-// search over supersets of Q4 gives 40 B/lane of scratch for DBL .. GM against 72 for all
-// programs and 136 for DBL .. Q4 or Q4 alone (tools/resource_table.py, guarded by
-// tests/test_resources.py)
+// register allocation as measured then); for k_line_prod (Q4I, Q4) the quad programs: a search
+// over supersets gives 28 B/lane of scratch with Q4SQ's cases in the switch against 40 without
+// them and up to 56 for other sets (tools/resource_table.py, guarded by tests/test_resources.py)
 #define ZG_PMASK_R4 0xffu
-#define ZG_LP_MASK 0x1ffu
+#define ZG_LP_MASK (ZG_PMASK(Q4SQ) | ZG_PMASK(Q4) | ZG_PMASK(Q4I))
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
   return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
@@ -346,16 +345,18 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
 //   prod_i f_i = chain_n (f <- (f L_n)^2 or f L_n).
 // The L_n of all steps are independent of each other: k_line_prod forms them at full occupancy
 // (lane = (step, group), Q4 programs f <- f l_4t l_4t+1 l_4t+2 l_4t+3 over the group's lines, 13
-// products per proof and step, no squaring) and the sequential part shrinks to one chain per
+// products per proof and step, no squaring; the first four lines from scratch, Q4I) and the sequential part shrinks to one chain per
 // group (k_batch_fchaing, GMSQ: 30 products per step for the whole group). Against the quad
 // chain (Q4SQ, 16 products per proof-step, all on the 68-step sequential path) that is 13 + 30 / G.
 // lprod layout: [n][6][m] (m = npad / G groups; coefficient-major, coalesced on lane = group).
-__device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int blk,
-                                              const AtomSpace& at) {
+// n0: the first step of this launch (the host launches the steps in parts, k_batch_fchaing
+// consuming each part while the next is formed)
+__device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
+                                              int blk, const AtomSpace& at) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const size_t m = (size_t)b.npad / gsize;
   const int bps = (int)((m + 63) / 64);
-  const int n = blk / bps;
+  const int n = n0 + blk / bps;
   const size_t g = (size_t)(blk % bps) * 64 + lane;
   const bool inb = g < m;
   const int p0 = inb ? (int)(g * gsize) : 0;
@@ -367,61 +368,70 @@ __device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lin
       at.put(6 + j, act ? src0[12 * t + j] : (j % 3 == 0 ? f2_one() : f2_zero()));
     }
   };
-  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
+  // the first four lines from scratch (Q4I: (l0 l1)(l2 l3), 27 products), then Q4 per four
   for (int t = 0; t < gsize / 4; t++) {
     load(t);
     __syncthreads();
-    prog_run<true, ZG_LP_MASK>(ZG_PROG_Q4, at);
+    const int pid = wave_uniform(t == 0 ? ZG_PROG_Q4I : ZG_PROG_Q4);
+    prog_run<true, ZG_LP_MASK>(pid, at);
     Fq2 v;
-    if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[ZG_PROG_Q4].go + wave, at);
+    if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[pid].go + wave, at);
     __syncthreads();
     if (wave < 6) at.put(wave, v);
   }
   if (wave < 6 && inb) lprod[((size_t)n * 6 + wave) * m + g] = at.get(wave);
 }
-// one Miller chain per group over its line products; writes the tree level of groups (m nodes)
-__device__ __forceinline__ void fchaing_body(const BatchBufs& b, const Fq2* lprod, int m, int blk, const AtomSpace& at) {
+// one Miller chain per group over its line products, steps [n0, n1): f from fstate ([6][m]; 1 when
+// n0 = 0), back to fstate, or (n1 = 68) conjugated into the tree level of groups (m nodes)
+__device__ __forceinline__ void fchaing_body(const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0, int n1,
+                                             int blk, const AtomSpace& at) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const int g = blk * 64 + lane;
   const bool inb = g < m;
+  const int gi = inb ? g : 0;
   auto load_l = [&](int n) {
     const int s = (wave + 2) & 7;
-    if (s < 6) at.put(6 + s, lprod[((size_t)n * 6 + s) * m + (inb ? g : 0)]);
+    if (s < 6) at.put(6 + s, lprod[((size_t)n * 6 + s) * m + gi]);
   };
-  if (wave < 6) at.put(wave, wave == 0 ? f2_one() : f2_zero());
-  load_l(0);
+  if (wave < 6) at.put(wave, n0 > 0 ? fstate[(size_t)wave * m + gi] : wave == 0 ? f2_one() : f2_zero());
+  if (n0 < n1) load_l(n0);
   __syncthreads();
   int n = 0;
-  for (int i = ZG_XH_TOP;; i--) {
+  for (int i = ZG_XH_TOP; n < n1; i--) {
     const bool last = i < 0;
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
-    for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
+    for (int pass = 0; pass < (addbit ? 2 : 1); pass++, n++) {
+      if (n < n0 || n >= n1) continue;
       const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_GM : ZG_PROG_GMSQ);
       prog_run<true, ZG_PMASK(GM) | ZG_PMASK(GMSQ)>(pid, at);
       Fq2 v;
       if (wave < 6) v = prog_output<ZG_PMASK(GM) | ZG_PMASK(GMSQ)>(PROG_INFO[pid].go + wave, at);
       __syncthreads();
-      n++;
       if (wave < 6) at.put(wave, v);
-      if (n < ZG_NCOEFF) load_l(n);
+      if (n + 1 < n1) load_l(n + 1);
       __syncthreads();
     }
-    if (last) break;
   }
   if (wave < 6 && inb) {
     Fq2 v = at.get(wave);
-    if (wave >= 3) v = f2_neg(v);  // conjugate (u < 0)
-    reinterpret_cast<Fq2*>(&b.ftree[m + g])[wave] = v;
+    if (n1 < ZG_NCOEFF) {
+      fstate[(size_t)wave * m + g] = v;
+    } else {
+      if (wave >= 3) v = f2_neg(v);  // conjugate (u < 0)
+      reinterpret_cast<Fq2*>(&b.ftree[m + g])[wave] = v;
+    }
   }
 }
 #if defined(ZG_TU_PROG_FCHAIN4)
-__global__ void __launch_bounds__(64 * ZG_FC_NW) k_line_prod(BatchBufs b, const Fq2* lines, Fq2* lprod, int gsize) {
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_line_prod(BatchBufs b, const Fq2* lines, Fq2* lprod, int gsize,
+                                                             int n0) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  lineprod_body(b, lines, lprod, gsize, blockIdx.x, AtomSpace{lds_atoms});
+  lineprod_body(b, lines, lprod, gsize, n0, blockIdx.x, AtomSpace{lds_atoms});
 }
-__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, const Fq2* lprod, int m) {
+__global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, const Fq2* lprod, Fq2* fstate, int m,
+                                                                 int n0, int n1) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  fchaing_body(b, lprod, m, blockIdx.x, AtomSpace{lds_atoms});
+  fchaing_body(b, lprod, fstate, m, n0, n1, blockIdx.x, AtomSpace{lds_atoms});
 }
 #endif
 #if defined(ZG_TU_PROG_FCHAIN4)
@@ -561,7 +571,7 @@ __global__ void __launch_bounds__(64) k_tree_c(BatchBufs b, int lo, const int* g
 }
 
 struct NodeBufs {
-  const int* nodes;  // M tree node ids
+  const int* nodes;  // M tree node ids (null: the root alone, the pipeline's own node list)
   G1J* msm;          // M x 3 x ZG_MSM_SLOTS
   Fq12* pairf;       // M x 3 x ZG_NPAIRS
   int* ok;           // M
@@ -581,7 +591,7 @@ __global__ void __launch_bounds__(64) k_node_msm(BatchBufs b, NodeBufs nb, const
   const int j = (t / ZG_SHIFTS) % ZG_MSM_SLOTS;
   const int kind = (t / (ZG_SHIFTS * ZG_MSM_SLOTS)) % ZG_NKINDS;
   const int idx = t / (ZG_SHIFTS * ZG_MSM_SLOTS * ZG_NKINDS);
-  const int node = nb.nodes[idx];
+  const int node = nb.nodes ? nb.nodes[idx] : 1;
   const DevVK& vk = b.vks[kind];
   G1J res = jac_infinity<Fq>();
   bool live = false;
@@ -698,7 +708,7 @@ __global__ void __launch_bounds__(64) k_node_pairs(BatchBufs b, NodeBufs nb, con
     k0 = p / ZG_NPAIRS;
     k1 = k0 + 1;
   }
-  const int node = nb.nodes[idx];
+  const int node = nb.nodes ? nb.nodes[idx] : 1;
   const DevVK& vk0 = b.vks[k0];  // (merged: gamma / alpha / beta are the same in every loaded key)
   // the G1 point of this pair: the sum of the keys' MSM partials (gamma pair: up to 3 x 10 x 8,
   // beta pair: 8), or the node's C sum (delta pair), summed across the wave (a few adds per lane
@@ -762,7 +772,7 @@ __global__ void __launch_bounds__(64) k_node_final(BatchBufs b, NodeBufs nb, int
   const int idx = blockIdx.x;
   if (idx >= nb.m) return;
   coop_init(&ws);
-  coop_load(&ws, 0, b.ftree[nb.nodes[idx]]);
+  coop_load(&ws, 0, b.ftree[nb.nodes ? nb.nodes[idx] : 1]);
   const int npn = b.merged ? ZG_NODE_PAIRS_MERGED : ZG_NODE_PAIRS;
   for (int p = 0; p < npn; p++) {
     const bool beta = b.merged ? p == npn - 1 : p % ZG_NPAIRS == 2;

@@ -14,15 +14,19 @@ hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs&
   hipLaunchKernelGGL(k_batch_fchain4, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines);
   return hipGetLastError();
 }
-// group line products, then one chain per group: m = npad / gsize groups (gsize a power of two >= 4)
-hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize) {
+// group line products of steps [n0, n1), then the groups' chains over them: m = npad / gsize groups
+// (gsize a power of two >= 4); fstate carries each chain's f between parts
+hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
+                                int n1) {
   const size_t m = (size_t)b.npad / gsize;
-  hipLaunchKernelGGL(k_line_prod, dim3((unsigned)(ZG_NCOEFF * ((m + 63) / 64))), dim3(64 * ZG_FC_NW), 0, st, b, lines,
-                     lprod, gsize);
+  hipLaunchKernelGGL(k_line_prod, dim3((unsigned)((n1 - n0) * ((m + 63) / 64))), dim3(64 * ZG_FC_NW), 0, st, b, lines,
+                     lprod, gsize, n0);
   return hipGetLastError();
 }
-hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, int m) {
-  hipLaunchKernelGGL(k_batch_fchaing, dim3((unsigned)((m + 63) / 64)), dim3(64 * ZG_FC_NW), 0, st, b, lprod, m);
+hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,
+                               int n1) {
+  hipLaunchKernelGGL(k_batch_fchaing, dim3((unsigned)((m + 63) / 64)), dim3(64 * ZG_FC_NW), 0, st, b, lprod, fstate, m,
+                     n0, n1);
   return hipGetLastError();
 }
 
