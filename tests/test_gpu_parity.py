@@ -137,7 +137,7 @@ def test_batch_4096_one_percent_corrupted(ctx):
 def test_batch_4096_corrupted_quad_fchain(ctx, monkeypatch, group):
     """the same 41-in-4,096 batch with the four-proofs-per-lane f-chain forced (ZG_FCHAIN_QUADS=1,
     split launches): the quad tree level has no pair nodes below it, and bisection must still
-    reach the exact reject set. group: ZG_LINE_GROUP -- default (below 65,536 proofs the quad chain),
+    reach the exact reject set. group: ZG_LINE_GROUP -- default (below 32,768 proofs the quad chain),
     32 (group line products of 32 proofs: no tree below the groups until bisection runs the quad
     chain), 4096 (one group: the chain writes the root)"""
     from zebra_amd import Context

@@ -38,7 +38,7 @@ using namespace zg;
 #define ZG_NTIMINGS 9
 #define ZG_NSTATS 12
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
-#define ZG_LINE_PROD_MIN 65536   // shards from this many padded proofs run the f-chain as group line products
+#define ZG_LINE_PROD_MIN 32768   // shards from this many padded proofs run the f-chain as group line products
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
 #define ZG_K4_MIN 16384          // lone batches from this many (padded) proofs sum r_i C_i by K4's Pippenger
                                  // buckets; smaller lone batches by the GLV products in decode + the C tree
@@ -841,9 +841,10 @@ static int run_pipeline(zg_ctx* ctx) {
   const bool quads = !fused && ctx->npad >= 4 && (ctx->quads == 1 || (ctx->quads < 0 && ctx->npad >= ZG_QUAD_MIN));
   ctx->quads_last = quads;
   // group line products (k_line_prod + k_batch_fchaing) instead of the quad chain: auto from
-  // ZG_LINE_PROD_MIN, 32 proofs a group (in flight, ms per batch, quad chain -> groups of 16 / 32 / 64:
-  // 64k 13.67 -> 12.97 / 12.75 / 12.90, 32k 7.26 -> 7.24 at 32 and 64, 16k 4.17 -> 4.38 at 32, 8k 2.63 -> 2.89
-  // at 32; profiles/r05p_lineprod_ab.txt)
+  // ZG_LINE_PROD_MIN, 32 proofs a group (in flight, ms per batch, quad chain -> line products with the
+  // chains in four parts, groups of 16 / 32 / 64 / 128: 64k 13.67 -> 12.84 / 12.69 / 12.72 / 13.05, 32k
+  // 7.33 -> 7.01 (64: 7.09), 16k 4.15 -> 4.20, 8k 2.63 -> 2.89 with one part;
+  // profiles/r05p_lineprod_ab.txt, r05v_lineprod_sweep.txt)
   int gsize = ctx->line_group < 0 ? (ctx->npad >= ZG_LINE_PROD_MIN ? 32 : 0) : ctx->line_group;
   if ((size_t)gsize > ctx->npad) gsize = 0;
   const bool lineprod = quads && gsize;
