@@ -476,6 +476,10 @@ def main():
     if os.path.exists(pmc) and shard == 65536 and not fused:   # the PMC passes run the default 64k bench
         pt = json.load(open(pmc))
         traffic, k4_traffic = pt.get(rk), pt.get("k_msm_bucket")
+        if "+" in rk:  # the line-product phase: each kernel runs once per step part (4 by default)
+            parts = int(os.environ.get("ZG_LINE_PROD_PARTS", "4"))
+            got = [pt.get(k) for k in rk.split("+")]
+            traffic = parts * sum(got) if all(g is not None for g in got) else None
     k4 = None
     if k4_entries is not None and iso_avg[8] > 0:
         npad = 1 << max(1, (shard - 1).bit_length())
