@@ -28,8 +28,8 @@ using namespace zg;
 
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
-#define ZG_NEV 19  // [13]: zg_gt_check; [14..17] line-product parts, [18] their chains done (no timing)
-#define ZG_LP_PARTS_MAX 4
+#define ZG_LP_PARTS_MAX 8
+#define ZG_NEV (15 + ZG_LP_PARTS_MAX)  // [13]: zg_gt_check; [14..] line-product parts, [14 + max] chains done (no timing)
 // the pinned host block of a context: the root's 576-B Miller partial, the pipeline flags
 // (bfail, fused-wait failure), the K4 entry count, then the n statuses
 #define ZG_PIN_FLAGS 576
@@ -173,7 +173,7 @@ struct zg_ctx {
   int line_group = -1;       // ZG_LINE_GROUP: proofs per group (k_line_prod): -1 auto (32 from ZG_LINE_PROD_MIN
                              // padded proofs, else the quad chain), 0 never, a power of two >= 4 always
   int lineprod_last = 0;     // the last batch's f-chain ran on group line products (no tree below the groups)
-  int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..4)
+  int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..8)
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
@@ -891,8 +891,8 @@ static int run_pipeline(zg_ctx* ctx) {
           HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[14 + k], 0));
           HIPCHK(launch_prog_fchaing(ctx->side, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, n0, n1));
         }
-        HIPCHK(hipEventRecord(ctx->ev[18], ctx->side));
-        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[18], 0));
+        HIPCHK(hipEventRecord(ctx->ev[14 + ZG_LP_PARTS_MAX], ctx->side));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[14 + ZG_LP_PARTS_MAX], 0));
       }
     } else if (quads) {
       HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines));
