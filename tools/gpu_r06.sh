@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 GPU pass: gpu tests, smoke, the driver's bench command (timed), optionally rocprofv3
-# kernel stats of the bench. Usage (repo root on the box): bash tools/gpu_r05.sh TAG [tests|bench|prof]...
+# Round-6 GPU pass: gpu tests, smoke, the driver's bench command (timed), optionally rocprofv3
+# kernel stats of the bench. Usage (repo root on the box): bash tools/gpu_r06.sh TAG [tests|bench|prof]...
 set -o pipefail
-TAG=${1:-r05}
+TAG=${1:-r06}
 shift
 STEPS=${*:-tests bench}
 R=$(pwd)

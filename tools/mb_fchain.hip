@@ -10,6 +10,9 @@
 #include <string.h>
 #include <vector>
 
+#ifndef ZG_MB_SPLIT
+#define ZG_MB_SPLIT true  // the product kernel's default (zg_kernels.h fchain4_body)
+#endif
 #ifdef ZG_FC_TRACE
 #define TRB 4               // traced blocks
 #define TRS 80              // events per step
@@ -108,7 +111,7 @@ int main(int argc, char** argv) {
   float best = 1e30f, sum = 0;
   for (int r = 0; r <= reps; r++) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_batch_fchain4, dim3(blocks), dim3(64 * ZG_FC_NW), 0, 0, b, (const Fq2*)lines);
+    hipLaunchKernelGGL(k_batch_fchain4<ZG_MB_SPLIT>, dim3(blocks), dim3(64 * ZG_FC_NW), 0, 0, b, (const Fq2*)lines);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;

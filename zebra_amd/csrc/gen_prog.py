@@ -308,6 +308,17 @@ def prog_q4i():
     return p, pair_pair(p, line_pair(p, ls[0], ls[1]), line_pair(p, ls[2], ls[3]))
 
 
+def prog_q4ik():
+    """the same four-line product with the accumulator f kept in slots 0..5 (k_line_prod's later
+    quads, the quad chain): the kernel stores the quad to slots 6..11 and multiplies it into f with
+    GM / GMSQ -- 27 + 18 products per four lines instead of Q4's 52 (27 + 30 instead of Q4SQ's 64)"""
+    p = Prog("q4ik", ["F%d" % i for i in range(6)] + ["%s%d" % (c, j) for j in range(4) for c in "ABC"],
+             keep=range(6))
+    ins = [p.inp(i) for i in range(18)]
+    ls = [ins[6 + 3 * j: 9 + 3 * j] for j in range(4)]
+    return p, pair_pair(p, line_pair(p, ls[0], ls[1]), line_pair(p, ls[2], ls[3]))
+
+
 # ---------------------------------------------------------------- scheduling + slots
 # Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
 # Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
@@ -498,7 +509,7 @@ def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False, fixed=None):
             free_at[s] = last.get(("p", i), nr) + shift
     # outputs are written to input slots 0.. after the output round: they must not clobber a
     # kept input
-    assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add")
+    assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add", "q4ik")
     return {"rounds": rounds, "slot": slot, "nslots": nslots, "rnd": rnd, "rb": int(shift == 0), "sinks": sinks}
 
 
@@ -935,7 +946,7 @@ def emit(specs):
     out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
                sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq", "q4i")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq", "q4i", "q4ik")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
     out.append("// program mask of a kernel: ZG_PMASK(A) | ZG_PMASK(B) ... (bit k: program ZG_PROG_* = k)")
     out.append("#define ZG_PMASK(P) (1u << ZG_PROG_##P)")
@@ -971,7 +982,8 @@ LINES_MAX_SLOTS = 13
 
 
 SCHED_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zg_prog_sched.json")
-SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "q4i": 3000, "dbl": 6000, "add": 6000}
+SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "q4i": 3000, "q4ik": 3000,
+          "dbl": 6000, "add": 6000}
 
 
 def build_all(search=None):
@@ -983,13 +995,13 @@ def build_all(search=None):
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
                    (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN),
-                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN), (prog_q4i, NW_FCHAIN)):
+                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN), (prog_q4i, NW_FCHAIN), (prog_q4ik, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
                                        prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
                                        prog_gm: (0, True, True, 25), prog_gmsq: (0, True, True, 25),
-                                       prog_q4i: (0, True, True, 25),
+                                       prog_q4i: (0, True, True, 25), prog_q4ik: (0, True, True, 25),
                                        prog_dbl: (0, True, True, LINES_MAX_SLOTS),
                                        prog_add: (0, True, True, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
         share = 1 if fn in (prog_dbl, prog_add) else 2

@@ -173,6 +173,8 @@ struct zg_ctx {
   int line_group = -1;       // ZG_LINE_GROUP: proofs per group (k_line_prod): -1 auto (32 from ZG_LINE_PROD_MIN
                              // padded proofs, else the quad chain), 0 never, a power of two >= 4 always
   int lineprod_last = 0;     // the last batch's f-chain ran on group line products (no tree below the groups)
+  int quad_split = 1;        // ZG_QUAD_SPLIT: 1 a step's four lines multiply first, then into f (Q4IK + GM / GMSQ,
+                             // round 6), 0 the fused Q4 / Q4SQ programs (same values)
   int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..8)
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
@@ -312,6 +314,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_SERIAL_SIDE")) ctx->serial_side = atoi(e);
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_LINE_GROUP")) ctx->line_group = atoi(e);
+  if (const char* e = getenv("ZG_QUAD_SPLIT")) ctx->quad_split = atoi(e) ? 1 : 0;
   if (const char* e = getenv("ZG_LINE_PROD_PARTS")) ctx->lp_parts = std::max(1, std::min(ZG_LP_PARTS_MAX, atoi(e)));
   if (ctx->line_group != -1 && (ctx->line_group < 4 || (ctx->line_group & (ctx->line_group - 1)))) ctx->line_group = 0;
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
@@ -736,9 +739,9 @@ hipError_t launch_prog_lines(unsigned groups, hipStream_t st, const BatchBufs& b
 hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines,
                                    const int* nodes, int m);
 hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
-hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines);
+hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, int split);
 hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
-                                int n1);
+                                int n1, int split);
 hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,
                                int n1);
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
@@ -881,12 +884,14 @@ static int run_pipeline(zg_ctx* ctx) {
       // behind the line products except for the last part
       const int m = (int)(ctx->npad / gsize), parts = ctx->lp_parts;
       if (parts <= 1) {
-        HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, 0, ZG_NCOEFF));
+        HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, 0, ZG_NCOEFF,
+                                          ctx->quad_split));
         HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, 0, ZG_NCOEFF));
       } else {
         for (int k = 0; k < parts; k++) {
           const int n0 = ZG_NCOEFF * k / parts, n1 = ZG_NCOEFF * (k + 1) / parts;
-          HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, n0, n1));
+          HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, n0, n1,
+                                            ctx->quad_split));
           HIPCHK(hipEventRecord(ctx->ev[14 + k], ctx->stream));
           HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[14 + k], 0));
           HIPCHK(launch_prog_fchaing(ctx->side, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, n0, n1));
@@ -895,7 +900,7 @@ static int run_pipeline(zg_ctx* ctx) {
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[14 + ZG_LP_PARTS_MAX], 0));
       }
     } else if (quads) {
-      HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines));
+      HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->quad_split));
     } else {
       HIPCHK(launch_prog_fchain(pgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, (const int*)nullptr));
     }
@@ -1221,7 +1226,8 @@ static int build_trees(zg_ctx* ctx) {
   // (still in HBM) and the levels above write every node (those from the groups up again, with
   // the same values)
   if (ctx->lineprod_last) {
-    HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines));
+    HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines,
+                               ctx->quad_split));
     HIPCHK(launch_f_tree(ctx, b, ctx->npad / 4));
   }
   HIPCHK(hipEventRecord(ctx->ev[10], ctx->stream));

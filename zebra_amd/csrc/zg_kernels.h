@@ -32,7 +32,9 @@ namespace zg {
 // over supersets gives 28 B/lane of scratch with Q4SQ's cases in the switch against 40 without
 // them and up to 56 for other sets (tools/resource_table.py, guarded by tests/test_resources.py)
 #define ZG_PMASK_R4 0xffu
-#define ZG_LP_MASK (ZG_PMASK(Q4SQ) | ZG_PMASK(Q4) | ZG_PMASK(Q4I))
+#ifndef ZG_LP_MASK
+#define ZG_LP_MASK (ZG_PMASK(Q4SQ) | ZG_PMASK(Q4) | ZG_PMASK(Q4I) | ZG_PMASK(Q4IK) | ZG_PMASK(GM))
+#endif
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
   return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
@@ -287,11 +289,15 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain(BatchBufs b, con
 #endif
 
 // Four proofs per lane (large shards, ZG_QUAD_MIN): the quad (4j .. 4j+3) shares one Miller
-// accumulator, f <- (f l_4j l_4j+1 l_4j+2 l_4j+3)^2 per step (staged programs Q4SQ / Q4: 64 Fq2
-// products per quad-step where two pairs need 76), and the kernel writes the tree level of proof
-// quads (npad/4 nodes; bisection never stops at the pair level below it, zg.hip bisect).
-// LDS slots 0..5 f, 6..17 the four line triples; atom j of a step's lines is loaded by wave
-// (j + 6) mod 8, alongside waves 0..5 storing the f outputs.
+// accumulator, f <- (f l_4j l_4j+1 l_4j+2 l_4j+3)^2 per step, and the kernel writes the tree level of
+// proof quads (npad/4 nodes; bisection never stops at the pair level below it, zg.hip bisect).
+// SPLIT (default, round 6): the step's four lines multiply first, (l0 l1)(l2 l3) by Q4IK (27 products,
+// f kept in slots 0..5), then the quad into f by GMSQ / GM -- 57 products per quad-step instead of the
+// fused Q4SQ's 64 (Q4: 45 instead of 52); !SPLIT: Q4SQ / Q4. Both give the same field elements.
+// LDS slots 0..5 f, 6..17 the four line triples (the quad in 6..11 between the two programs); atom j of
+// a step's lines is loaded by wave (j + 6) mod 8, alongside waves 0..5 storing the f outputs.
+#define ZG_FC4_MASK (ZG_PMASK_R4 | ZG_PMASK(GM) | ZG_PMASK(GMSQ) | ZG_PMASK(Q4IK))
+template <bool SPLIT>
 __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* lines, int blk, const AtomSpace& at) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
   const int quad = blk * 64 + lane;
@@ -314,12 +320,24 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
     const bool last = i < 0;
     const bool addbit = !last && ((ZG_XH >> i) & 1ull);
     for (int pass = 0; pass < (addbit ? 2 : 1); pass++) {
-      const int pid = wave_uniform((last || (addbit && pass == 0)) ? ZG_PROG_Q4 : ZG_PROG_Q4SQ);
-      ZG_TRACE_S(n, 0);
-      prog_run<true, ZG_PMASK_R4>(pid, at);
-      ZG_TRACE_S(n, 1);
+      const bool sq = !(last || (addbit && pass == 0));
       Fq2 v;
-      if (wave < 6) v = prog_output<ZG_PMASK_R4>(PROG_INFO[pid].go + wave, at);
+      ZG_TRACE_S(n, 0);
+      if constexpr (SPLIT) {
+        prog_run<true, ZG_FC4_MASK>(ZG_PROG_Q4IK, at);
+        if (wave < 6) v = prog_output<ZG_FC4_MASK>(PROG_INFO[ZG_PROG_Q4IK].go + wave, at);
+        __syncthreads();
+        if (wave < 6) at.put(6 + wave, v);
+        __syncthreads();
+        const int pid = wave_uniform(sq ? ZG_PROG_GMSQ : ZG_PROG_GM);
+        prog_run<true, ZG_FC4_MASK>(pid, at);
+        if (wave < 6) v = prog_output<ZG_FC4_MASK>(PROG_INFO[pid].go + wave, at);
+      } else {
+        const int pid = wave_uniform(sq ? ZG_PROG_Q4SQ : ZG_PROG_Q4);
+        prog_run<true, ZG_FC4_MASK>(pid, at);
+        if (wave < 6) v = prog_output<ZG_FC4_MASK>(PROG_INFO[pid].go + wave, at);
+      }
+      ZG_TRACE_S(n, 1);
       ZG_TRACE_S(n, 2);
       __syncthreads();
       ZG_TRACE_S(n, 3);
@@ -351,6 +369,7 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
 // lprod layout: [n][6][m] (m = npad / G groups; coefficient-major, coalesced on lane = group).
 // n0: the first step of this launch (the host launches the steps in parts, k_batch_fchaing
 // consuming each part while the next is formed)
+template <bool SPLIT>
 __device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
                                               int blk, const AtomSpace& at) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
@@ -368,15 +387,24 @@ __device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lin
       at.put(6 + j, act ? src0[12 * t + j] : (j % 3 == 0 ? f2_one() : f2_zero()));
     }
   };
-  // the first four lines from scratch (Q4I: (l0 l1)(l2 l3), 27 products), then Q4 per four
+  // the first four lines from scratch (Q4I: (l0 l1)(l2 l3), 27 products); then per four lines
+  // SPLIT: the quad by Q4IK (27, f kept in slots 0..5) into slots 6..11, times f by GM (18): 45
+  // products instead of Q4's 52
   for (int t = 0; t < gsize / 4; t++) {
     load(t);
     __syncthreads();
-    const int pid = wave_uniform(t == 0 ? ZG_PROG_Q4I : ZG_PROG_Q4);
+    const int pid = wave_uniform(t == 0 ? ZG_PROG_Q4I : SPLIT ? ZG_PROG_Q4IK : ZG_PROG_Q4);
     prog_run<true, ZG_LP_MASK>(pid, at);
     Fq2 v;
     if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[pid].go + wave, at);
     __syncthreads();
+    if (SPLIT && t > 0) {  // the quad into f
+      if (wave < 6) at.put(6 + wave, v);
+      __syncthreads();
+      prog_run<true, ZG_LP_MASK>(ZG_PROG_GM, at);
+      if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[ZG_PROG_GM].go + wave, at);
+      __syncthreads();
+    }
     if (wave < 6) at.put(wave, v);
   }
   if (wave < 6 && inb) lprod[((size_t)n * 6 + wave) * m + g] = at.get(wave);
@@ -423,10 +451,11 @@ __device__ __forceinline__ void fchaing_body(const BatchBufs& b, const Fq2* lpro
   }
 }
 #if defined(ZG_TU_PROG_FCHAIN4)
+template <bool SPLIT>
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_line_prod(BatchBufs b, const Fq2* lines, Fq2* lprod, int gsize,
                                                              int n0) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  lineprod_body(b, lines, lprod, gsize, n0, blockIdx.x, AtomSpace{lds_atoms});
+  lineprod_body<SPLIT>(b, lines, lprod, gsize, n0, blockIdx.x, AtomSpace{lds_atoms});
 }
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, const Fq2* lprod, Fq2* fstate, int m,
                                                                  int n0, int n1) {
@@ -435,9 +464,10 @@ __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, co
 }
 #endif
 #if defined(ZG_TU_PROG_FCHAIN4)
+template <bool SPLIT>
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchain4(BatchBufs b, const Fq2* lines) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  fchain4_body(b, lines, blockIdx.x, AtomSpace{lds_atoms});
+  fchain4_body<SPLIT>(b, lines, blockIdx.x, AtomSpace{lds_atoms});
 }
 #endif
 

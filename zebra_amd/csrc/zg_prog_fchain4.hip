@@ -10,17 +10,24 @@
 
 namespace zg {
 
-hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines) {
-  hipLaunchKernelGGL(k_batch_fchain4, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines);
+// split: the four lines' product first, then into f (Q4IK + GMSQ / GM; zg_kernels.h fchain4_body)
+hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, int split) {
+  if (split)
+    hipLaunchKernelGGL(k_batch_fchain4<true>, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines);
+  else
+    hipLaunchKernelGGL(k_batch_fchain4<false>, dim3(blocks), dim3(64 * ZG_FC_NW), 0, st, b, lines);
   return hipGetLastError();
 }
 // group line products of steps [n0, n1), then the groups' chains over them: m = npad / gsize groups
 // (gsize a power of two >= 4); fstate carries each chain's f between parts
 hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
-                                int n1) {
+                                int n1, int split) {
   const size_t m = (size_t)b.npad / gsize;
-  hipLaunchKernelGGL(k_line_prod, dim3((unsigned)((n1 - n0) * ((m + 63) / 64))), dim3(64 * ZG_FC_NW), 0, st, b, lines,
-                     lprod, gsize, n0);
+  const dim3 grid((unsigned)((n1 - n0) * ((m + 63) / 64)));
+  if (split)
+    hipLaunchKernelGGL(k_line_prod<true>, grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
+  else
+    hipLaunchKernelGGL(k_line_prod<false>, grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
   return hipGetLastError();
 }
 hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,
