@@ -204,9 +204,11 @@ PGHR13_FQ_PER_PROOF = {"g1_decode": 2205, "g2_decode": 2570, "input_combs": 3312
                        "p7": 1470, "b_lines": 3312, "segment_loops": 4674}
 
 
-def other_configs(ctx, src_proofs, src_kinds, reps=5):
+def other_configs(ctx, src_proofs, src_kinds, cpu_threads=0, reps=5):
     """SURVEY.md 8(d) configs 2 and 4 through the host-buffer API zg_verify_batch (PCIe copies,
-    OS-RNG scalars and the exact per-proof statuses included): not the headline metric."""
+    OS-RNG scalars and the exact per-proof statuses included), the clean 4,096 batch config 4 is set
+    against, and config 5 through the block collector (tools/bench_config5.py, with the C++
+    restatement on the same blocks when cpu_threads): not the headline metric."""
     import random
     real = {e["name"]: e for e in json.load(open(os.path.join(ROOT, "tests", "golden", "real_proofs.json")))["proofs"]}
     pts = json.load(open(os.path.join(ROOT, "tests", "golden", "points.json")))
@@ -257,6 +259,19 @@ def other_configs(ctx, src_proofs, src_kinds, reps=5):
     assert sts == want, "config 4 reject set differs"
     res["config4_4096_1pct_corrupted"] = {"proofs_per_s": n / dt, "ms_per_batch": dt * 1e3, "rejected": len(bad),
                                           "exact_reject_set": True}
+    # the same 4,096 proofs uncorrupted: what config 4's bisection is set against
+    clean = ctx.synth_rerandomize(src_proofs, src_kinds, idx, 3)
+    cin = pack_inputs([rows[srcs[j]] for j in idx])
+    ctx.verify_batch(clean, kinds, cin)
+    t = time.perf_counter()
+    for _ in range(reps):
+        sts, _ = ctx.verify_batch(clean, kinds, cin)
+    dt4 = (time.perf_counter() - t) / reps
+    assert sts == [0] * n
+    res["clean_4096_ms"] = dt4 * 1e3
+    res["config4_over_clean_4096"] = dt / dt4
+    from tools import bench_config5
+    res["config5_replay"] = bench_config5.run(ctx, cpu_threads)
     return res
 
 
@@ -532,7 +547,7 @@ def main():
                               "verdict": "sync" if args.sync_verdict else "deferred (worker thread, checker context)"},
     }
     if rank == 0 and world == 1 and not args.no_configs:
-        out["other_configs"] = other_configs(ctx, src_proofs, src_kinds)
+        out["other_configs"] = other_configs(ctx, src_proofs, src_kinds, 0 if args.no_cpu else cpu_threads(args.cpu_threads))
         # note-commitment tree windows (tools/bench_tree.py), not the headline
         from tools import bench_tree
         from zebra_amd import zg as _zg

@@ -142,10 +142,12 @@ int zg_batch_begin(zg_ctx* ctx, size_t n, const uint8_t* proofs, const uint8_t* 
 int zg_batch_begin_device(zg_ctx* ctx, size_t n, const void* d_proofs, const void* d_kinds,
                           const void* d_inputs, const void* d_n_inputs, const void* d_r);
 int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
-/* zg_batch_ready: 1 when the batch begun on ctx has finished its device work (zg_batch_partial and
- * a true-verdict zg_batch_finish then return without waiting), 0 while it runs, < 0 on error. It
- * never blocks: a host loop keeping several batches in flight harvests whichever finishes first
- * (batches in flight finish out of order). */
+/* zg_batch_ready: 1 when the batch begun on ctx has finished its pipeline (zg_batch_partial and a
+ * true-verdict zg_batch_finish then return without waiting -- unless a B_i failed its G2 subgroup
+ * check: the root sums then still hold that proof and zg_batch_partial first recomputes them and
+ * the partial, synchronously), 0 while it runs, < 0 on error. It never blocks: a host loop keeping
+ * several batches in flight harvests whichever finishes first (batches in flight finish out of
+ * order). */
 int zg_batch_ready(zg_ctx* ctx);
 int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
 int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);

@@ -42,7 +42,7 @@ def test_prog_schedule_structure():
             assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
             # B and C (outputs 4, 5) leave through their products' waves: no slot
             assert sorted(sch["sinks"].values()) == [4, 5], name
-        elif name in ("q4sq", "q4", "gm", "gmsq", "q4i"):
+        elif name in ("q4sq", "q4", "gm", "gmsq", "q4i", "q4ik"):
             # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse (and the
             # group chain's general products run in the same LDS budget, k_batch_fchaing)
             assert sch["nslots"] <= 25 and sch["rb"] == 1, name
@@ -95,6 +95,14 @@ def test_fchain_programs():
             ((ls[2][0], ls[2][1], B.F2_ZERO), (B.F2_ZERO, ls[2][2], B.F2_ZERO))),
             ((ls[3][0], ls[3][1], B.F2_ZERO), (B.F2_ZERO, ls[3][2], B.F2_ZERO))))
         assert run("q4sq", f12_pairs(f) + flat) == f12_pairs(B.f12_sqr(f4))
+        # the same four-line product with f kept in its slots (the split quad step, round 6): the
+        # kernel then multiplies it into f with GM / GMSQ, which gives Q4 / Q4SQ's values
+        prog, outs, sch = progs()["q4ik"]
+        assert all(sch["slot"][("in", i)] == i for i in range(6)) and set(prog.keep) == set(range(6))
+        quad = run("q4ik", f12_pairs(f) + flat)
+        assert quad == run("q4i", f12_pairs(f) + flat)
+        assert run("gm", f12_pairs(f) + quad) == f12_pairs(f4)
+        assert run("gmsq", f12_pairs(f) + quad) == f12_pairs(B.f12_sqr(f4))
         # the group chain (k_batch_fchaing): f * L and (f * L)^2 for a general Fq12 L (the product
         # of a group's lines at one step, k_line_prod)
         g = B.f12_from_coeffs([rng.randrange(P) for _ in range(12)])

@@ -29,7 +29,9 @@ using namespace zg;
 #define ZG_BLOCK 64
 #define ZG_NODE_CHUNK 4096
 #define ZG_LP_PARTS_MAX 8
-#define ZG_NEV (15 + ZG_LP_PARTS_MAX)  // [13]: zg_gt_check; [14..] line-product parts, [14 + max] chains done (no timing)
+#define ZG_EV_SETTLE (15 + ZG_LP_PARTS_MAX)  // settle_batch's recompute (no timing)
+#define ZG_NEV (16 + ZG_LP_PARTS_MAX)  // [13]: zg_gt_check; [14..] line-product parts, [14 + max] chains done,
+                                       // [15 + max] settle_batch (no timing)
 // the pinned host block of a context: the root's 576-B Miller partial, the pipeline flags
 // (bfail, fused-wait failure), the K4 entry count, then the n statuses
 #define ZG_PIN_FLAGS 576
@@ -342,8 +344,12 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   A(dalloc(&ctx->d_ptB, cap));
   A(dalloc(&ctx->d_ftree, 2 * (size_t)cap));
   A(dalloc(&ctx->d_lines, (size_t)cap * ZG_NCOEFF * 3));
-  if (ctx->line_group) A(dalloc(&ctx->d_lprod, ((size_t)cap / 4 + 1) * ZG_NCOEFF * 6));
-  if (ctx->line_group) A(dalloc(&ctx->d_fstate, ((size_t)cap / 4 + 1) * 6));
+  // group line products: sized for the smallest group that can run on this context (an explicit
+  // ZG_LINE_GROUP, else the automatic 32 from ZG_LINE_PROD_MIN padded proofs; none below that)
+  const uint32_t lp_gmin = ctx->line_group > 0 ? (uint32_t)ctx->line_group
+                                                : ctx->line_group < 0 && cap >= ZG_LINE_PROD_MIN ? 32u : 0u;
+  if (lp_gmin) A(dalloc(&ctx->d_lprod, ((size_t)cap / lp_gmin + 1) * ZG_NCOEFF * 6));
+  if (lp_gmin) A(dalloc(&ctx->d_fstate, ((size_t)cap / lp_gmin + 1) * 6));
   A(dalloc(&ctx->d_ctree, 2 * (size_t)cap * ZG_NKINDS));
   A(dalloc(&ctx->d_stree, 2 * (size_t)cap * ZG_NKINDS * ZG_MAX_IC));
   A(dalloc(&ctx->msm.count, ZG_MSM_NCOUNT_MAX));
@@ -849,7 +855,7 @@ static int run_pipeline(zg_ctx* ctx) {
   // 7.33 -> 7.01 (64: 7.09), 16k 4.15 -> 4.20, 8k 2.63 -> 2.89 with one part;
   // profiles/r05p_lineprod_ab.txt, r05v_lineprod_sweep.txt)
   int gsize = ctx->line_group < 0 ? (ctx->npad >= ZG_LINE_PROD_MIN ? 32 : 0) : ctx->line_group;
-  if ((size_t)gsize > ctx->npad) gsize = 0;
+  if ((size_t)gsize > ctx->npad || !ctx->d_lprod) gsize = 0;  // (d_lprod: zg_create sized it for this gsize)
   const bool lineprod = quads && gsize;
   ctx->lineprod_last = lineprod;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
@@ -1075,9 +1081,10 @@ static int check_nodes(zg_ctx* ctx, const std::vector<int>& nodes, int mode, std
   return ZG_OK;
 }
 
-// after the batch's device work: timings and the pipeline's flags (B subgroup failures that
-// forced the gated recompute; a fused launch whose consumers timed out waiting, which turns
-// the fused shape off for this context)
+// after the batch's device work: timings and the pipeline's flags (B subgroup failures, whose root
+// sums settle_batch recomputed; a fused launch whose consumers timed out waiting, which turns
+// the fused shape off for this context). The timings are the pipeline's own (ev[0..10]): the
+// settle recompute waits on an event of its own and is not in them.
 static int collect_batch_stats(zg_ctx* ctx) {
   int flags[2] = {0, 0}, entries = 0;
   HIPCHK(wait_event(ctx->ev[4]));  // the pipeline's last step (run_pipeline)
@@ -1099,7 +1106,7 @@ static int collect_batch_stats(zg_ctx* ctx) {
   hipEventElapsedTime(&ctx->timings[2], ctx->ev[7], ctx->ev[2]);  // f-chain
   hipEventElapsedTime(&ctx->timings[3], ctx->ev[2], ctx->ev[3]);  // Fq12 product tree
   hipEventElapsedTime(&ctx->timings[4], ctx->ev[3], ctx->ev[4]);  // root partial: waits for the side stream
-                                                                  // (serial_side: runs it), gated recompute
+                                                                  // (serial_side: runs it)
   hipEventElapsedTime(&ctx->timings[5], ctx->ev[5], ctx->ev[6]);  // side stream: trees + VK-side root work
   hipEventElapsedTime(&ctx->timings[6], ctx->ev[0], ctx->ev[4]);  // whole device pipeline
   hipEventElapsedTime(&ctx->timings[7], ctx->ev[5], ctx->ev[10]);  // K4 (Pippenger + root Fr sums)
@@ -1129,8 +1136,9 @@ static int settle_batch(zg_ctx* ctx) {
   hipLaunchKernelGGL(k_f12_to_bytes, dim3(1), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_out, 1, ctx->d_bytes);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ctx->h_pin, ctx->d_bytes, 576, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
-  HIPCHK(wait_event(ctx->ev[4]));
+  // its own event: ev[4] stays the pipeline's end (collect_batch_stats' timings)
+  HIPCHK(hipEventRecord(ctx->ev[ZG_EV_SETTLE], ctx->stream));
+  HIPCHK(wait_event(ctx->ev[ZG_EV_SETTLE]));
   return ZG_OK;
 }
 

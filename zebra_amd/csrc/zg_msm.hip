@@ -145,9 +145,9 @@ __global__ void __launch_bounds__(ZG_MSM_BT) k_msm_bucket(BatchBufs b, MsmBufs m
     const int bucket = gw * BS + j;
     const int lo = m.start[bucket], len = m.start[bucket + 1] - lo;
     const int beg = lo + len * part / P, end = lo + len * (part + 1) / P;
-    // (an entry past what k_msm_scatter wrote can only be stale when k_batch_lines flipped a
-    // status between count and scatter -- then bfail > 0 and the gated recompute redoes it; it
-    // must still stay inside the buffers). The next entry's operands are gathered while the
+    // (an entry past what k_msm_scatter wrote can only be stale when the R-chain flipped a
+    // status between count and scatter -- then bfail > 0 and settle_batch (zg.hip) recomputes the
+    // root sums on the host's request; it must still stay inside the buffers). The next entry's operands are gathered while the
     // current one is added: their L2 / HBM latency hides behind the addition.
     auto entry = [&](int e) { return staged ? st[e - slo] : m.entries[e]; };
     auto gather = [&](uint32_t ent, FqD* x, FqD* y) {
