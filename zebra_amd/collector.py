@@ -90,9 +90,61 @@ class Tx:
     binding_sig: Optional[bytes] = None
 
 
+_POOL = None
+_PAR_MIN = 32   # prep jobs below this run inline (a pool round trip costs more than they do)
+
+
+def _prep_pool():
+    """host threads for the public-input preparation (Jubjub point decodes, small-order checks,
+    multipacking: ~0.35 ms of C per Sapling description); the prep functions are ctypes calls into
+    libzg.so, which release the GIL, so a window's descriptions decode in parallel like the
+    reference's rayon fan-out over transactions (accept_chain.rs:76-81). Sized like the bench's
+    CPU share: OMP_NUM_THREADS when set, else every usable CPU (at most 64)."""
+    global _POOL
+    if _POOL is None:
+        import concurrent.futures
+        import os
+        try:
+            n = len(os.sched_getaffinity(0))
+        except AttributeError:
+            n = os.cpu_count() or 1
+        omp = os.environ.get("OMP_NUM_THREADS", "")
+        if omp.isdigit() and int(omp) > 0:
+            n = min(n, int(omp))
+        _POOL = concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(64, n)))
+    return _POOL
+
+
+def _run_prep(job):
+    fn, args = job
+    try:
+        return fn(*args)
+    except zg.PrepError as e:
+        return e
+
+
 def _queue(txs):
     """prepare inputs; returns (Groth16 items, PGHR13 items, per-tx plans). A plan entry refers
-    to a queued proof by index ("proof" / "pghr"), or carries a prep error or a caller verdict."""
+    to a queued proof by index ("proof" / "pghr"), or carries a prep error or a caller verdict.
+    The prep calls of the whole window run first (in parallel for a large window), then the
+    items and plans are assembled in reference order."""
+    jobs = []
+    for tx in txs:
+        for d in tx.joinsplits:
+            if tx.js_pubkey is None or (not d.groth and d.pghr_ok is not None):
+                continue
+            fn = zg.prep_joinsplit if d.groth else zg.prep_joinsplit_bn
+            jobs.append((fn, (d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old, d.vpub_new,
+                              tx.js_pubkey)))
+        for s in tx.spends:
+            jobs.append((zg.prep_spend, (s.cv, s.anchor, s.nullifier, s.rk)))
+        for o in tx.outputs:
+            jobs.append((zg.prep_output, (o.cv, o.cmu, o.epk)))
+    if len(jobs) >= _PAR_MIN:
+        done = list(_prep_pool().map(_run_prep, jobs, chunksize=16))
+    else:
+        done = [_run_prep(j) for j in jobs]
+    res = iter(done)
     items, pghr, plans = [], [], []
     for tx in txs:
         js_plan, sp_plan, out_plan = [], [], []
@@ -100,29 +152,26 @@ def _queue(txs):
             if tx.js_pubkey is None or (not d.groth and d.pghr_ok is not None):
                 js_plan.append(("caller", bool(d.pghr_ok)))
                 continue
+            inp = next(res)
+            if isinstance(inp, zg.PrepError):   # (the JoinSplit preps raise no PrepError)
+                raise inp
             if not d.groth:
-                inp = zg.prep_joinsplit_bn(d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments,
-                                           d.vpub_old, d.vpub_new, tx.js_pubkey)
                 js_plan.append(("pghr", len(pghr)))
                 pghr.append((bytes(d.zkproof), inp))
                 continue
-            inp = zg.prep_joinsplit(d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old,
-                                    d.vpub_new, tx.js_pubkey)
             js_plan.append(("proof", len(items)))
             items.append((zg.KIND_SPROUT, bytes(d.zkproof), inp))
         for s in tx.spends:
-            try:
-                inp = zg.prep_spend(s.cv, s.anchor, s.nullifier, s.rk)
-            except zg.PrepError as e:
-                sp_plan.append(("prep", e.name))
+            inp = next(res)
+            if isinstance(inp, zg.PrepError):
+                sp_plan.append(("prep", inp.name))
                 continue
             sp_plan.append(("proof", len(items)))
             items.append((zg.KIND_SPEND, bytes(s.zkproof), inp))
         for o in tx.outputs:
-            try:
-                inp = zg.prep_output(o.cv, o.cmu, o.epk)
-            except zg.PrepError as e:
-                out_plan.append(("prep", e.name))
+            inp = next(res)
+            if isinstance(inp, zg.PrepError):
+                out_plan.append(("prep", inp.name))
                 continue
             out_plan.append(("proof", len(items)))
             items.append((zg.KIND_OUTPUT, bytes(o.zkproof), inp))

@@ -39,7 +39,62 @@ ZG_HD inline Fr prep_fr_const(const uint32_t* c) {
   for (int i = 0; i < 8; i++) r.l[i] = c[i];
   return r;
 }
-ZG_HD inline Fr prep_fr_sqr(const Fr& a) { return fr_mul(a, a); }
+#if defined(__HIP_DEVICE_COMPILE__)
+ZG_HD inline Fr prep_fr_mul(const Fr& a, const Fr& b) { return fr_mul(a, b); }
+#else
+// the host's product: 4 x 64-bit CIOS over unsigned __int128, the same Montgomery form (R = 2^256) and
+// the same canonical result as fr_mul's 8 x 32-bit words -- ~10x faster on the host, where a window's
+// descriptions are prepared (two Jubjub decodes per Sapling description, ~1,100 products each)
+inline Fr prep_fr_mul(const Fr& a, const Fr& b) {
+  static constexpr uint64_t M[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                    0x73eda753299d7d48ull};
+  static constexpr uint64_t INV = 0xfffffffeffffffffull;  // -r^-1 mod 2^64
+  typedef unsigned __int128 u128;
+  uint64_t x[4], y[4], t[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    x[i] = a.l[2 * i] | (uint64_t)a.l[2 * i + 1] << 32;
+    y[i] = b.l[2 * i] | (uint64_t)b.l[2 * i + 1] << 32;
+  }
+  for (int i = 0; i < 4; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < 4; j++) {
+      const u128 p = (u128)x[j] * y[i] + t[j] + c;
+      t[j] = (uint64_t)p;
+      c = (uint64_t)(p >> 64);
+    }
+    u128 s = (u128)t[4] + c;
+    t[4] = (uint64_t)s;
+    const uint64_t t5 = (uint64_t)(s >> 64);
+    const uint64_t m = t[0] * INV;
+    u128 p = (u128)m * M[0] + t[0];
+    c = (uint64_t)(p >> 64);
+    for (int j = 1; j < 4; j++) {
+      p = (u128)m * M[j] + t[j] + c;
+      t[j - 1] = (uint64_t)p;
+      c = (uint64_t)(p >> 64);
+    }
+    s = (u128)t[4] + c;
+    t[3] = (uint64_t)s;
+    t[4] = t5 + (uint64_t)(s >> 64);
+  }
+  // t < 2r: one conditional subtraction
+  uint64_t d[4], bw = 0;
+  for (int j = 0; j < 4; j++) {
+    const u128 q = (u128)t[j] - M[j] - bw;
+    d[j] = (uint64_t)q;
+    bw = (uint64_t)(q >> 64) & 1u;
+  }
+  const bool ge = t[4] || !bw;
+  Fr r;
+  for (int i = 0; i < 4; i++) {
+    const uint64_t v = ge ? d[i] : t[i];
+    r.l[2 * i] = (uint32_t)v;
+    r.l[2 * i + 1] = (uint32_t)(v >> 32);
+  }
+  return r;
+}
+#endif
+ZG_HD inline Fr prep_fr_sqr(const Fr& a) { return prep_fr_mul(a, a); }
 ZG_HD inline Fr prep_fr_sub(const Fr& a, const Fr& b) { return fp_sub<FrM>(a, b); }
 ZG_HD inline Fr prep_fr_neg(const Fr& a) { return fp_neg<FrM>(a); }
 ZG_HD inline bool prep_fr_eq(const Fr& a, const Fr& b) { return fp_eq<FrM>(a, b); }
@@ -47,13 +102,13 @@ ZG_HD inline Fr prep_fr_pow(const Fr& a, const uint32_t* e, int nbits) {
   Fr r = fr_one();
   for (int i = nbits - 1; i >= 0; i--) {
     r = prep_fr_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1u) r = fr_mul(r, a);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = prep_fr_mul(r, a);
   }
   return r;
 }
 ZG_HD inline Fr prep_fr_inv(const Fr& a) { return prep_fr_pow(a, FR_EXP_INV, 255); }
 
-// Tonelli-Shanks (r - 1 = 2^32 t); returns false for a non-residue. Any root: the caller fixes
+// Tonelli-Shanks (r - 1 = 2^32 t); returns false for a non-residue (detected by the order search). Any root: the caller fixes
 // the sign from the encoding.
 ZG_HD inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
   if (fp_is_zero<FrM>(a)) {
@@ -61,11 +116,9 @@ ZG_HD inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
     return true;
   }
   const Fr one = fr_one();
-  // legendre
-  if (!prep_fr_eq(prep_fr_pow(a, FR_EXP_LEGENDRE, 255), one)) return false;
   Fr w = prep_fr_pow(a, FR_TS_TM1_2, 223);  // a^((t-1)/2)
-  Fr x = fr_mul(a, w);                      // a^((t+1)/2)
-  Fr b = fr_mul(x, w);                      // a^t
+  Fr x = prep_fr_mul(a, w);                      // a^((t+1)/2)
+  Fr b = prep_fr_mul(x, w);                      // a^t
   Fr z = prep_fr_const(FR_TS_ROOT);
   int v = 32;
   while (!prep_fr_eq(b, one)) {
@@ -74,12 +127,16 @@ ZG_HD inline bool prep_fr_sqrt(const Fr& a, Fr* out) {
     while (!prep_fr_eq(b2k, one)) {
       b2k = prep_fr_sqr(b2k);
       k++;
+      // a non-residue: b = a^t has order exactly 2^32 (a^((r-1)/2) = -1), so the order search
+      // reaches v = 32 on the first pass; a residue's never does (this replaces the Legendre
+      // exponentiation the round-1 code ran first)
+      if (k >= v) return false;
     }
     Fr ww = z;
     for (int j = 0; j < v - k - 1; j++) ww = prep_fr_sqr(ww);
     z = prep_fr_sqr(ww);
-    b = fr_mul(b, z);
-    x = fr_mul(x, ww);
+    b = prep_fr_mul(b, z);
+    x = prep_fr_mul(x, ww);
     v = k;
   }
   *out = x;
@@ -111,9 +168,9 @@ ZG_HD inline bool jubjub_read(const uint8_t* in, JubjubPt* p) {
   y = fr_to_mont(y);
   const Fr y2 = prep_fr_sqr(y);
   const Fr num = prep_fr_sub(y2, fr_one());
-  const Fr den = fr_add(fr_mul(prep_fr_const(JUBJUB_D), y2), fr_one());
+  const Fr den = fr_add(prep_fr_mul(prep_fr_const(JUBJUB_D), y2), fr_one());
   Fr x;
-  if (!prep_fr_sqrt(fr_mul(num, prep_fr_inv(den)), &x)) return false;  // not on curve
+  if (!prep_fr_sqrt(prep_fr_mul(num, prep_fr_inv(den)), &x)) return false;  // not on curve
   const Fr xc = fr_from_mont(x);
   if ((bool)(xc.l[0] & 1u) != sign) x = prep_fr_neg(x);
   p->x = x;
@@ -132,9 +189,9 @@ ZG_HD inline bool jubjub_is_small_order(const JubjubPt& p) {
     const Fr F = fr_add(E, D);
     const Fr H = prep_fr_sqr(Z);
     const Fr J = prep_fr_sub(F, fr_add(H, H));
-    X = fr_mul(prep_fr_sub(prep_fr_sub(B, C), D), J);
-    Y = fr_mul(F, prep_fr_sub(E, D));
-    Z = fr_mul(F, J);
+    X = prep_fr_mul(prep_fr_sub(prep_fr_sub(B, C), D), J);
+    Y = prep_fr_mul(F, prep_fr_sub(E, D));
+    Z = prep_fr_mul(F, J);
   }
   return fp_is_zero<FrM>(X) && prep_fr_eq(Y, Z);
 }
