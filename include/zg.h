@@ -297,7 +297,7 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
 /* cumulative counters of this context: [0] batches, [1] fused R-chain + f-chain launches,
  * [2] fused launches whose consumers timed out waiting (the f-chain was recomputed by the
  * split kernel; the context uses split launches from then on), [3] batches with a B that
- * failed its G2 subgroup check (gated recompute of the VK-side root work), [4] bisections,
+ * failed its G2 subgroup check (the VK-side root work recomputed at harvest, settle_batch), [4] bisections,
  * [5] tree nodes checked by bisection, [6] K4 bucket entries of the last batch (points with a
  * non-zero window digit, summed over the windows), [7] f-chain launches with four proofs per lane
  * (k_batch_fchain4; shards of 8,192 or more padded proofs -- ZG_QUAD_MIN -- or as ZG_FCHAIN_QUADS
@@ -307,7 +307,8 @@ int zg_last_phase_ms(zg_ctx* ctx, float* ms, size_t n);
  * from the GLV products in decode and the C-sum tree (shards below 16,384 padded proofs -- ZG_K4_MIN
  * -- instead of K4's Pippenger buckets; [6] is 0 for them), [11] of the four-proofs-per-lane batches
  * ([7]) those whose f-chain ran as group line products + one chain per group (k_line_prod,
- * k_batch_fchaing; ZG_LINE_GROUP proofs a group). Writes min(n, 12) values, zero beyond. */
+ * k_batch_fchaing; ZG_LINE_GROUP proofs a group), [12] of those the batches whose lines came from the affine
+ * R-chain (k_batch_lines_aff, ZG_LINES_AFFINE). Writes min(n, 13) values, zero beyond. */
 int zg_stats(zg_ctx* ctx, uint64_t* out, size_t n);
 /* the batch-scalar CSPRNG (contexts with seeded = 0): per batch a fresh 256-bit key from
  * getrandom(2), expanded on the device by ChaCha20 (RFC 8439), nonce 0, block j -> r_{4j..4j+3}.

@@ -664,6 +664,69 @@ def miller_loop(pairs):
     return f12_conj(f)
 
 
+# --- affine G2 lines normalised to a unit vw coefficient (zebra_amd's ZG_LINES_AFFINE path; test
+# infrastructure). The line through R with slope lambda, evaluated at p = (px, py), is pairing's
+# `ell` operand up to a factor in Fq2 * Fq: (lambda x_R - y_R) + (-lambda px) v + py v w. Divided by py:
+#   a + b v + v w,  a = (lambda x_R - y_R) / py,  b = -lambda px / py.
+# The final exponentiation kills Fq2 and Fq factors (p^6 - 1 divides its exponent), so a Miller value
+# over these lines has the same GT image as miller_loop's; the 576-B partial is a different element.
+def affine_lines(q, p):
+    """G2Prepared(q)'s 68 steps in affine coordinates with the lines for p normalised: [(a, b)]"""
+    px, py = p
+    ipy = fq_inv(py)
+    pxy = px * ipy % P
+    qx, qy = q
+    x, y = q
+    out = []
+
+    def step(x, y, dbl):
+        if dbl:
+            lam = f2_mul(f2_scale(f2_sqr(x), 3), f2_inv(f2_scale(y, 2)))
+            x3 = f2_sub(f2_sqr(lam), f2_scale(x, 2))
+        else:
+            lam = f2_mul(f2_sub(qy, y), f2_inv(f2_sub(qx, x)))
+            x3 = f2_sub(f2_sub(f2_sqr(lam), x), qx)
+        y3 = f2_sub(f2_mul(lam, f2_sub(x, x3)), y)
+        out.append((f2_scale(f2_sub(f2_mul(lam, x), y), ipy), f2_neg(f2_scale(lam, pxy))))
+        return x3, y3
+    for bit in _X_BITS:
+        x, y = step(x, y, True)
+        if bit == '1':
+            x, y = step(x, y, False)
+    step(x, y, True)
+    return out
+
+
+def _aline(ab):
+    a, b = ab
+    return ((a, b, F2_ZERO), (F2_ZERO, F2_ONE, F2_ZERO))
+
+
+AFFINE_IDLE_LINE = (F2_ZERO, F2_ZERO)   # the line v w (= w^3, FE-trivial) a slot without a proof contributes
+
+
+def miller_chain_affine(lines_list):
+    """the Miller chain over the products of several proofs' normalised lines (one list of 68 (a, b)
+    per proof, AFFINE_IDLE_LINE lists for empty slots), conjugated (u < 0): the group chain of
+    k_line_prod / k_batch_fchaing on affine lines"""
+    f = F12_ONE
+    n = 0
+
+    def mul_step(f, n):
+        for ls in lines_list:
+            f = f12_mul(f, _aline(ls[n]))
+        return f
+    for bit in _X_BITS:
+        f = mul_step(f, n)
+        n += 1
+        if bit == '1':
+            f = mul_step(f, n)
+            n += 1
+        f = f12_sqr(f)
+    f = mul_step(f, n)
+    return f12_conj(f)
+
+
 def _exp_by_x(f, x):
     return f12_conj(f12_pow(f, x))
 

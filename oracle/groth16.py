@@ -185,12 +185,17 @@ def batch_gt(lhs_list, r_list):
     return acc
 
 
-def batch_partial(pvks, items):
+def batch_partial(pvks, items, affine_slots=None):
     """The Miller partial F of a shard, exactly as the GPU forms it (not final-exponentiated):
     prod_i ML(r_i A_i, B_i) * prod_k ML(acc_k, -gamma_k) ML(Csum_k, -delta_k) ML(-S_k alpha_k, beta_k)
     over proofs that decode with a well-formed VK -- with the gamma and beta pairs merged across
-    keys that share alpha, beta, gamma. items: (kind, proof bytes, inputs, r)."""
+    keys that share alpha, beta, gamma. items: (kind, proof bytes, inputs, r).
+    affine_slots (the GPU's affine-line path, ZG_LINES_AFFINE): the proofs' Miller values from the
+    unit-normalised affine lines (B.affine_lines), and every one of the affine_slots (npad) proof slots
+    without a live proof -- padding, decode-invalid, malformed -- contributing the chain of the line v w
+    (B.AFFINE_IDLE_LINE), as the group line products form them."""
     f = B.F12_ONE
+    live = 0
     sums = {k: [0] * len(p.ic) for k, p in pvks.items()}
     csum = {k: None for k in pvks}
     for kind, pb, inputs, r in items:
@@ -204,11 +209,18 @@ def batch_partial(pvks, items):
         pvk = pvks[kind]
         if len(inputs) + 1 != len(pvk.ic):
             continue
-        f = B.f12_mul(f, B.miller_loop([(B.ec_mul(B.FQ, a, r), B.g2_prepare(b))]))
+        if affine_slots:
+            f = B.f12_mul(f, B.miller_chain_affine([B.affine_lines(b, B.ec_mul(B.FQ, a, r))]))
+        else:
+            f = B.f12_mul(f, B.miller_loop([(B.ec_mul(B.FQ, a, r), B.g2_prepare(b))]))
+        live += 1
         sums[kind][0] = (sums[kind][0] + r) % B.R
         for j, x in enumerate(inputs):
             sums[kind][j + 1] = (sums[kind][j + 1] + r * x) % B.R
         csum[kind] = B.ec_add(B.FQ, csum[kind], B.ec_mul(B.FQ, c, r))
+    if affine_slots:
+        idle = B.miller_chain_affine([[B.AFFINE_IDLE_LINE] * 68])
+        f = B.f12_mul(f, B.f12_pow(idle, affine_slots - live))
     # keys sharing alpha, beta and gamma (the three Zcash keys): FE is bilinear, so the GPU merges
     # their gamma pairs into ONE (sum_k acc_k, -gamma) and their beta pairs into ONE
     # (-(sum_k S_k0) alpha, beta) next to one delta pair per key (zebra_amd/csrc/zg_batch.h)

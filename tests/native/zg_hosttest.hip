@@ -121,6 +121,37 @@ void zgt_lines_lane(const uint8_t* q, const uint8_t* p, uint8_t* out_lane, uint8
   }
 }
 
+// the affine R-chain step of zg_lines.h (k_batch_lines_aff's ls_aff_step) for one proof, with every
+// denominator inverted directly (the kernel batches them by Montgomery's trick): 68 (a, b) pairs of
+// the unit-normalised lines, Fq2 as c0 || c1 BE, and the final affine point [x] B (x.c0 x.c1 y.c0 y.c1)
+void zgt_lines_affine(const uint8_t* q, const uint8_t* p, uint8_t* out, uint8_t* last) {
+  G2A B = {{ld_fq(q), ld_fq(q + 48)}, {ld_fq(q + 96), ld_fq(q + 144)}, false};
+  const Fq px = ld_fq(p), py = ld_fq(p + 48);
+  const Fq ipy = fq_inv(py);
+  const Fq2 ab = {ipy, fq_mul(px, ipy)};
+  Fq2 x = B.x, y = B.y;
+  int n = 0;
+  auto step = [&](bool dbl) {
+    const Fq2 d = dbl ? f2_dbl(y) : f2_sub(B.x, x);
+    const Fq ninv = fq_inv(ls_norm(d));
+    Fq2 a, b;
+    ls_aff_step(x, y, &B, dbl, ninv, ab, &a, &b);
+    st_fq(a.c0, out + (n * 2) * 96);
+    st_fq(a.c1, out + (n * 2) * 96 + 48);
+    st_fq(b.c0, out + (n * 2 + 1) * 96);
+    st_fq(b.c1, out + (n * 2 + 1) * 96 + 48);
+    n++;
+  };
+  for (int i = ZG_XH_TOP; i >= -1; i--) {
+    step(true);
+    if (i >= 0 && ((ZG_XH >> i) & 1ull)) step(false);
+  }
+  st_fq(x.c0, last);
+  st_fq(x.c1, last + 48);
+  st_fq(y.c0, last + 96);
+  st_fq(y.c1, last + 144);
+}
+
 // the products of zg_debug_field_mul (zebra_amd/csrc/zg_debug.hip) on the host: same field ids
 void zgt_field_mul(int field, const uint32_t* a, const uint32_t* b, uint32_t* r) {
   switch (field) {

@@ -231,6 +231,38 @@ def test_lines_lane_equals_g2_prepared(L):
         assert a.raw == r.raw
 
 
+def test_affine_lines_equal_oracle(L):
+    """the affine R-chain step of zg_lines.h (k_batch_lines_aff, ZG_LINES_AFFINE) gives the oracle's
+    unit-normalised lines (oracle/bls12_381.py affine_lines) for all 68 steps, and ends at [x] B; the
+    oracle's lines are pairing's projective lines up to Fq2 * Fq factors (same GT image,
+    test_affine_miller_value_has_the_pairing_gt)"""
+    import ctypes
+    rng = random.Random(32)
+    for _ in range(3):
+        q = B.ec_mul(B.FQ2, B.G2_GEN, rng.randrange(1, B.R))
+        p = B.ec_mul(B.FQ, B.G1_GEN, rng.randrange(1, B.R))
+        qb = b"".join(fq_b(v) for v in (q[0][0], q[0][1], q[1][0], q[1][1]))
+        pb = fq_b(p[0]) + fq_b(p[1])
+        out, last = ctypes.create_string_buffer(68 * 2 * 96), ctypes.create_string_buffer(192)
+        L.zgt_lines_affine(qb, pb, out, last)
+        want = b"".join(fq_b(c) for ab in B.affine_lines(q, p) for f in ab for c in f)
+        assert out.raw == want
+        xq = B.ec_mul(B.FQ2, q, B.BLS_X)
+        assert last.raw == b"".join(fq_b(v) for v in (xq[0][0], xq[0][1], xq[1][0], xq[1][1]))
+
+
+def test_affine_miller_value_has_the_pairing_gt():
+    """the Miller chain over unit-normalised affine lines has the projective miller_loop's final
+    exponentiation (the normalisations are Fq2 * Fq factors), and the idle line v w maps to 1"""
+    rng = random.Random(33)
+    q = B.ec_mul(B.FQ2, B.G2_GEN, rng.randrange(1, B.R))
+    p = B.ec_mul(B.FQ, B.G1_GEN, rng.randrange(1, B.R))
+    fa = B.miller_chain_affine([B.affine_lines(q, p)])
+    fp = B.miller_loop([(p, B.g2_prepare(q))])
+    assert fa != fp and B.final_exponentiation(fa) == B.final_exponentiation(fp)
+    assert B.final_exponentiation(B.miller_chain_affine([[B.AFFINE_IDLE_LINE] * 68])) == B.F12_ONE
+
+
 def test_msm_windows_cover_the_scalar_evenly():
     """K4's signed-digit windows (zg_msm.h msm_shape / msm_digit, k_msm_count / k_msm_scatter):
     for every shard shape the digits reconstruct the 65-bit k0 and the 64-bit k1 exactly with a

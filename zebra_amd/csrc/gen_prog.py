@@ -319,6 +319,28 @@ def prog_q4ik():
     return p, pair_pair(p, line_pair(p, ls[0], ls[1]), line_pair(p, ls[2], ls[3]))
 
 
+def aline_pair(p, l, l2, one):
+    """the product of two affine lines normalised to a unit vw coefficient, (a + b v + v w)(a' + b' v + v w)
+    = (a a' + xi + (a b' + a' b) v + b b' v^2) + ((a + a') v + (b + b') v^2) w (w^2 = v, v^3 = xi): 3
+    products, in line_pair's layout (E0, E1, E2, E4, E5); `one` is an atom holding 1 (the xi term)"""
+    a, b = l
+    a2, b2 = l2
+    aa, bb = p.mul(a, a2), p.mul(b, b2)
+    return [aa + one.nr(), p.mul(a + b, a2 + b2) - aa - bb, bb, a + a2, b + b2]
+
+
+def prog_aq4():
+    """four affine lines (k_line_prod over the affine R-chain's lines, ZG_LINES_AFFINE): (l0 l1)(l2 l3)
+    with unit-normalised lines l = a + b v + v w, 3 + 3 + 15 = 21 products (Q4I: 27). in: F0..F5 (kept:
+    the group's accumulator), a0 b0 .. a3 b3, ONE (kept: the constant 1)."""
+    p = Prog("aq4", ["F%d" % i for i in range(6)] + ["%s%d" % (c, j) for j in range(4) for c in "ab"] + ["ONE"],
+             keep=list(range(6)) + [14])
+    ins = [p.inp(i) for i in range(15)]
+    ls = [ins[6 + 2 * j: 8 + 2 * j] for j in range(4)]
+    one = ins[14]
+    return p, pair_pair(p, aline_pair(p, ls[0], ls[1], one), aline_pair(p, ls[2], ls[3], one))
+
+
 # ---------------------------------------------------------------- scheduling + slots
 # Cost model (clocks of one SIMD, gfx950, measured with tools/mb_fq29 and tools/mb_rates): an
 # Fq2 product in 29-bit digits is ~8,600 (x*y, 1,171 v_mad_u64_u32) or ~6,500 (square, x*Fq);
@@ -509,7 +531,7 @@ def _schedule(prog, outs, nw, rng, slack, shift=1, partial=False, fixed=None):
             free_at[s] = last.get(("p", i), nr) + shift
     # outputs are written to input slots 0.. after the output round: they must not clobber a
     # kept input
-    assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add", "q4ik")
+    assert all(j not in prog.keep for j in range(len(outs)) if j < nin) or prog.name in ("dbl", "add", "q4ik", "aq4")
     return {"rounds": rounds, "slot": slot, "nslots": nslots, "rnd": rnd, "rb": int(shift == 0), "sinks": sinks}
 
 
@@ -946,7 +968,7 @@ def emit(specs):
     out.append("#define ZG_LINES_SINK_MASK 0x%x  // lines outputs stored by their products" %
                sum(1 << j for j in lsinks[0]))
     for name, nslots in (("LINES", max(i[9] for i in infos if i[0] in ("dbl", "add"))),
-                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq", "q4i", "q4ik")))):
+                         ("FCHAIN", max(i[9] for i in infos if i[0] in ("msq", "m", "mmsq", "mm", "q4sq", "q4", "gm", "gmsq", "q4i", "q4ik", "aq4")))):
         out.append("#define ZG_%s_SLOTS %d" % (name, nslots))
     out.append("// program mask of a kernel: ZG_PMASK(A) | ZG_PMASK(B) ... (bit k: program ZG_PROG_* = k)")
     out.append("#define ZG_PMASK(P) (1u << ZG_PROG_##P)")
@@ -983,6 +1005,7 @@ LINES_MAX_SLOTS = 13
 
 SCHED_CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "zg_prog_sched.json")
 SEARCH = {"mmsq": 3000, "mm": 3000, "q4sq": 3000, "q4": 3000, "gm": 3000, "gmsq": 3000, "q4i": 3000, "q4ik": 3000,
+          "aq4": 3000,
           "dbl": 6000, "add": 6000}
 
 
@@ -995,13 +1018,15 @@ def build_all(search=None):
     specs = []
     for fn, nw in ((prog_dbl, NW_LINES), (prog_add, NW_LINES), (prog_msq, NW_FCHAIN), (prog_m, NW_FCHAIN),
                    (prog_mmsq, NW_FCHAIN), (prog_mm, NW_FCHAIN), (prog_q4sq, NW_FCHAIN), (prog_q4, NW_FCHAIN),
-                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN), (prog_q4i, NW_FCHAIN), (prog_q4ik, NW_FCHAIN)):
+                   (prog_gm, NW_FCHAIN), (prog_gmsq, NW_FCHAIN), (prog_q4i, NW_FCHAIN), (prog_q4ik, NW_FCHAIN),
+                   (prog_aq4, NW_FCHAIN)):
         prog, outs = fn()
         # the two-proof programs must fit the one-proof f-chain's LDS (25 slots x 6 KB)
         shift, partial, cost, slots = {prog_mmsq: (1, False, True, 25), prog_mm: (1, False, True, 25),
                                        prog_q4sq: (0, True, True, 25), prog_q4: (0, True, True, 25),
                                        prog_gm: (0, True, True, 25), prog_gmsq: (0, True, True, 25),
                                        prog_q4i: (0, True, True, 25), prog_q4ik: (0, True, True, 25),
+                                       prog_aq4: (0, True, True, 25),
                                        prog_dbl: (0, True, True, LINES_MAX_SLOTS),
                                        prog_add: (0, True, True, LINES_MAX_SLOTS)}.get(fn, (1, False, False, None))
         share = 1 if fn in (prog_dbl, prog_add) else 2

@@ -38,7 +38,7 @@ using namespace zg;
 #define ZG_PIN_ENTRIES 584
 #define ZG_PIN_STATUS 640
 #define ZG_NTIMINGS 9
-#define ZG_NSTATS 12
+#define ZG_NSTATS 13
 #define ZG_TREE_COOP_BELOW 4096  // product-tree levels with fewer nodes run one wave per node
 #define ZG_LINE_PROD_MIN 32768   // shards from this many padded proofs run the f-chain as group line products
 #define ZG_QUAD_MIN 8192         // shards from this many (padded) proofs run the f-chain four proofs per lane (r02z: -4% at 16k, -1% at 8k)
@@ -175,6 +175,10 @@ struct zg_ctx {
   int line_group = -1;       // ZG_LINE_GROUP: proofs per group (k_line_prod): -1 auto (32 from ZG_LINE_PROD_MIN
                              // padded proofs, else the quad chain), 0 never, a power of two >= 4 always
   int lineprod_last = 0;     // the last batch's f-chain ran on group line products (no tree below the groups)
+  int lines_affine = 0;      // ZG_LINES_AFFINE: K (2, 4, 8) -- the group line products run on affine lines from
+                             // k_batch_lines_aff, K proofs per lane (round 6); 0 projective
+  int lines_affine_xl = 0;   // ZG_LINES_AFFINE_XL=1: its cross-lane variant (one inversion per wave; K = 4)
+  int affine_last = 0;       // the last batch's lines are affine (bisection re-forms projective ones)
   int quad_split = 1;        // ZG_QUAD_SPLIT: 1 a step's four lines multiply first, then into f (Q4IK + GM / GMSQ,
                              // round 6), 0 the fused Q4 / Q4SQ programs (same values)
   int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..8)
@@ -317,6 +321,12 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_FCHAIN_QUADS")) ctx->quads = atoi(e);
   if (const char* e = getenv("ZG_LINE_GROUP")) ctx->line_group = atoi(e);
   if (const char* e = getenv("ZG_QUAD_SPLIT")) ctx->quad_split = atoi(e) ? 1 : 0;
+  if (const char* e = getenv("ZG_LINES_AFFINE")) {
+    const int k = atoi(e);
+    ctx->lines_affine = k == 2 || k == 4 || k == 8 ? k : 0;
+  }
+  if (const char* e = getenv("ZG_LINES_AFFINE_XL")) ctx->lines_affine_xl = atoi(e) ? 1 : 0;
+  if (ctx->lines_affine_xl) ctx->lines_affine = 4;
   if (const char* e = getenv("ZG_LINE_PROD_PARTS")) ctx->lp_parts = std::max(1, std::min(ZG_LP_PARTS_MAX, atoi(e)));
   if (ctx->line_group != -1 && (ctx->line_group < 4 || (ctx->line_group & (ctx->line_group - 1)))) ctx->line_group = 0;
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
@@ -747,7 +757,8 @@ hipError_t launch_prog_leaf_fchain(unsigned blocks, hipStream_t st, const BatchB
 hipError_t launch_prog_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, const int* gate);
 hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs& b, const Fq2* lines, int split);
 hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
-                                int n1, int split);
+                                int n1, int split, int affine);
+hipError_t launch_lines_aff(hipStream_t st, const BatchBufs& b, Fq2* lines, int k, int xl);  // zg_lines.hip
 hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,
                                int n1);
 hipError_t launch_prog_lines_fchain(unsigned blocks, hipStream_t st, const BatchBufs& b, Fq2* lines, int* prog,
@@ -858,6 +869,10 @@ static int run_pipeline(zg_ctx* ctx) {
   if ((size_t)gsize > ctx->npad || !ctx->d_lprod) gsize = 0;  // (d_lprod: zg_create sized it for this gsize)
   const bool lineprod = quads && gsize;
   ctx->lineprod_last = lineprod;
+  // affine R-chain (ZG_LINES_AFFINE = K proofs per lane): only for the group line products, whose AQ4
+  // program reads its (a, b) lines; bisection re-forms projective lines for the chains below the groups
+  const bool affine = lineprod && ctx->lines_affine;
+  ctx->affine_last = affine;
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
@@ -872,7 +887,9 @@ static int run_pipeline(zg_ctx* ctx) {
     }
   } else {
     const bool lane = ctx->lines_lane > 0 || (ctx->lines_lane < 0 && ctx->npad >= ZG_LINES_LANE_MIN);
-    if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
+    if (affine) {  // affine lines for the group line products (zg_lines.hip k_batch_lines_aff)
+      HIPCHK(launch_lines_aff(ctx->stream, b, ctx->d_lines, ctx->lines_affine, ctx->lines_affine_xl));
+    } else if (lane) {  // lane = proof, straight-line products (zg_lines.hip)
       // register budget: auto sizes for one wave per SIMD (512 VGPRs: 64k alone 3.70 -> 3.38 ms) when no
       // other batch is on the device, else two (in flight the SIMDs' second slot serves the other
       // batches' kernels: 4 in flight 14.93 vs 14.47 ms per batch; profiles/r03c_bench_lines_lane*.json)
@@ -891,13 +908,13 @@ static int run_pipeline(zg_ctx* ctx) {
       const int m = (int)(ctx->npad / gsize), parts = ctx->lp_parts;
       if (parts <= 1) {
         HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, 0, ZG_NCOEFF,
-                                          ctx->quad_split));
+                                          ctx->quad_split, affine));
         HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, 0, ZG_NCOEFF));
       } else {
         for (int k = 0; k < parts; k++) {
           const int n0 = ZG_NCOEFF * k / parts, n1 = ZG_NCOEFF * (k + 1) / parts;
           HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, n0, n1,
-                                            ctx->quad_split));
+                                            ctx->quad_split, affine));
           HIPCHK(hipEventRecord(ctx->ev[14 + k], ctx->stream));
           HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[14 + k], 0));
           HIPCHK(launch_prog_fchaing(ctx->side, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, n0, n1));
@@ -1094,6 +1111,7 @@ static int collect_batch_stats(zg_ctx* ctx) {
   if (ctx->fused_last) ctx->stats[1]++;
   if (ctx->quads_last) ctx->stats[7]++;
   if (ctx->lineprod_last) ctx->stats[11]++;
+  if (ctx->affine_last) ctx->stats[12]++;
   if (flags[1]) {
     ctx->stats[2]++;
     ctx->fuse_off = 1;
@@ -1234,6 +1252,9 @@ static int build_trees(zg_ctx* ctx) {
   // (still in HBM) and the levels above write every node (those from the groups up again, with
   // the same values)
   if (ctx->lineprod_last) {
+    // affine lines: the chains below the groups read projective triples -- re-form them (the lane
+    // R-chain; its G2 checks repeat the affine chain's verdicts, every B already settled)
+    if (ctx->affine_last) HIPCHK(launch_lines_lane((unsigned)((ctx->npad + 63) / 64), ctx->stream, b, ctx->d_lines, 2));
     HIPCHK(launch_prog_fchain4((unsigned)((ctx->npad / 4 + 63) / 64), ctx->stream, b, (const Fq2*)ctx->d_lines,
                                ctx->quad_split));
     HIPCHK(launch_f_tree(ctx, b, ctx->npad / 4));

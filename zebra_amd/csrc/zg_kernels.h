@@ -35,6 +35,9 @@ namespace zg {
 #ifndef ZG_LP_MASK
 #define ZG_LP_MASK (ZG_PMASK(Q4SQ) | ZG_PMASK(Q4) | ZG_PMASK(Q4I) | ZG_PMASK(Q4IK) | ZG_PMASK(GM))
 #endif
+#ifndef ZG_LPA_MASK  // k_line_prod over affine lines (AQ4 + GM)
+#define ZG_LPA_MASK (ZG_PMASK(AQ4) | ZG_PMASK(GM))
+#endif
 
 __device__ __forceinline__ bool proof_active(const BatchBufs& b, int i) {
   return i < b.n && b.status[i] == ST_PENDING && !b.ptA[i].inf;
@@ -369,7 +372,10 @@ __device__ __forceinline__ void fchain4_body(const BatchBufs& b, const Fq2* line
 // lprod layout: [n][6][m] (m = npad / G groups; coefficient-major, coalesced on lane = group).
 // n0: the first step of this launch (the host launches the steps in parts, k_batch_fchaing
 // consuming each part while the next is formed)
-template <bool SPLIT>
+// AFF (ZG_LINES_AFFINE): the lines are the affine R-chain's unit-normalised pairs (a, b), lines[n][2][npad]
+// (zg_lines.hip k_batch_lines_aff): four lines are 8 atoms (slots 6..13, the constant 1 in slot 14) and
+// their product is AQ4 (21 products); a proof without a line contributes (0, 0), the FE-trivial v w.
+template <bool SPLIT, bool AFF>
 __device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
                                               int blk, const AtomSpace& at) {
   const int lane = threadIdx.x & 63, wave = wave_uniform(threadIdx.x >> 6);
@@ -381,28 +387,36 @@ __device__ __forceinline__ void lineprod_body(const BatchBufs& b, const Fq2* lin
   const int p0 = inb ? (int)(g * gsize) : 0;
   const Fq2* src0 = lines + ((size_t)n * b.npad + p0) * 3;
   // the lines of proofs p0 + 4t .. p0 + 4t + 3 into slots 6..17 (atom j by wave (j + 6) mod 8)
+  // (AFF: atom j = coefficient j % 2 of proof j / 2 into slot 6 + j by wave j, the 1 by wave 0)
   auto load = [&](int t) {
-    for (int j = (wave + 2) & 7; j < 12; j += 8) {
-      const bool act = inb && proof_active(b, p0 + 4 * t + j / 3);
-      at.put(6 + j, act ? src0[12 * t + j] : (j % 3 == 0 ? f2_one() : f2_zero()));
+    if constexpr (AFF) {
+      const int j = wave, pr = p0 + 4 * t + j / 2;
+      const bool act = inb && proof_active(b, pr);
+      at.put(6 + j, act ? lines[((size_t)n * 2 + (j & 1)) * b.npad + pr] : f2_zero());
+      if (wave == 0) at.put(14, f2_one());
+    } else {
+      for (int j = (wave + 2) & 7; j < 12; j += 8) {
+        const bool act = inb && proof_active(b, p0 + 4 * t + j / 3);
+        at.put(6 + j, act ? src0[12 * t + j] : (j % 3 == 0 ? f2_one() : f2_zero()));
+      }
     }
   };
   // the first four lines from scratch (Q4I: (l0 l1)(l2 l3), 27 products); then per four lines
   // SPLIT: the quad by Q4IK (27, f kept in slots 0..5) into slots 6..11, times f by GM (18): 45
-  // products instead of Q4's 52
+  // products instead of Q4's 52 (AFF: AQ4, 21 + 18)
   for (int t = 0; t < gsize / 4; t++) {
     load(t);
     __syncthreads();
-    const int pid = wave_uniform(t == 0 ? ZG_PROG_Q4I : SPLIT ? ZG_PROG_Q4IK : ZG_PROG_Q4);
-    prog_run<true, ZG_LP_MASK>(pid, at);
+    const int pid = wave_uniform(AFF ? ZG_PROG_AQ4 : t == 0 ? ZG_PROG_Q4I : SPLIT ? ZG_PROG_Q4IK : ZG_PROG_Q4);
+    prog_run<true, AFF ? ZG_LPA_MASK : ZG_LP_MASK>(pid, at);
     Fq2 v;
-    if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[pid].go + wave, at);
+    if (wave < 6) v = prog_output<AFF ? ZG_LPA_MASK : ZG_LP_MASK>(PROG_INFO[pid].go + wave, at);
     __syncthreads();
-    if (SPLIT && t > 0) {  // the quad into f
+    if ((SPLIT || AFF) && t > 0) {  // the quad into f
       if (wave < 6) at.put(6 + wave, v);
       __syncthreads();
-      prog_run<true, ZG_LP_MASK>(ZG_PROG_GM, at);
-      if (wave < 6) v = prog_output<ZG_LP_MASK>(PROG_INFO[ZG_PROG_GM].go + wave, at);
+      prog_run<true, AFF ? ZG_LPA_MASK : ZG_LP_MASK>(ZG_PROG_GM, at);
+      if (wave < 6) v = prog_output<AFF ? ZG_LPA_MASK : ZG_LP_MASK>(PROG_INFO[ZG_PROG_GM].go + wave, at);
       __syncthreads();
     }
     if (wave < 6) at.put(wave, v);
@@ -451,11 +465,11 @@ __device__ __forceinline__ void fchaing_body(const BatchBufs& b, const Fq2* lpro
   }
 }
 #if defined(ZG_TU_PROG_FCHAIN4)
-template <bool SPLIT>
+template <bool SPLIT, bool AFF>
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_line_prod(BatchBufs b, const Fq2* lines, Fq2* lprod, int gsize,
                                                              int n0) {
   __shared__ uint4 lds_atoms[ZG_FCHAIN_SLOTS * ZG_ATOM_ROWS * 64];
-  lineprod_body<SPLIT>(b, lines, lprod, gsize, n0, blockIdx.x, AtomSpace{lds_atoms});
+  lineprod_body<SPLIT, AFF>(b, lines, lprod, gsize, n0, blockIdx.x, AtomSpace{lds_atoms});
 }
 __global__ void __launch_bounds__(64 * ZG_FC_NW) k_batch_fchaing(BatchBufs b, const Fq2* lprod, Fq2* fstate, int m,
                                                                  int n0, int n1) {

@@ -20,14 +20,17 @@ hipError_t launch_prog_fchain4(unsigned blocks, hipStream_t st, const BatchBufs&
 }
 // group line products of steps [n0, n1), then the groups' chains over them: m = npad / gsize groups
 // (gsize a power of two >= 4); fstate carries each chain's f between parts
+// split: Q4IK + GM per four lines (else Q4); affine: the lines are the affine R-chain's (a, b) pairs (AQ4 + GM)
 hipError_t launch_prog_lineprod(hipStream_t st, const BatchBufs& b, const Fq2* lines, Fq2* lprod, int gsize, int n0,
-                                int n1, int split) {
+                                int n1, int split, int affine) {
   const size_t m = (size_t)b.npad / gsize;
   const dim3 grid((unsigned)((n1 - n0) * ((m + 63) / 64)));
-  if (split)
-    hipLaunchKernelGGL(k_line_prod<true>, grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
+  if (affine)
+    hipLaunchKernelGGL((k_line_prod<true, true>), grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
+  else if (split)
+    hipLaunchKernelGGL((k_line_prod<true, false>), grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
   else
-    hipLaunchKernelGGL(k_line_prod<false>, grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
+    hipLaunchKernelGGL((k_line_prod<false, false>), grid, dim3(64 * ZG_FC_NW), 0, st, b, lines, lprod, gsize, n0);
   return hipGetLastError();
 }
 hipError_t launch_prog_fchaing(hipStream_t st, const BatchBufs& b, const Fq2* lprod, Fq2* fstate, int m, int n0,

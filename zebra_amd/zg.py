@@ -306,7 +306,7 @@ class Context:
 
     STAT_NAMES = ("batches", "fused_launches", "fused_wait_failures", "b_subgroup_recomputes", "bisections",
                   "bisect_nodes", "k4_entries", "quad_fchain_launches", "pghr13_calls", "pghr13_batch_failures",
-                  "glv_csum_batches", "line_product_batches")
+                  "glv_csum_batches", "line_product_batches", "affine_line_batches")
 
     def stats(self):
         """cumulative counters (include/zg.h zg_stats) as a dict"""
