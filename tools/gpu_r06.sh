@@ -173,6 +173,16 @@ for s in $STEPS; do
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace ${PROFARGS:-} -d $O/occ8k -o run -- python3 $R/bench.py --no-cpu --no-configs --no-iso --proofs ${OCCN:-8192} --steps 36 --warmup 6 ${OCCARGS:-} > $O/occ8k.json 2> $O/occ8k.err || { echo "rocprof occ failed"; tail -30 $O/occ8k.err; exit 1; }
     cd $R && python3 tools/wavetime.py $O/occ8k/run_results.db $O/wavetime_occ.txt > /dev/null && python3 tools/occupancy.py $O/occ8k/run_results.db $O/occupancy.txt > $O/occupancy_stdout.txt && python3 tools/batch_path.py $O/occ8k/run_results.db $O/batch_path.txt > /dev/null && head -12 $O/occupancy.txt && head -40 $O/batch_path.txt && head -12 $O/wavetime_occ.txt && { [ -z "${PROFARGS:-}" ] || python3 tools/host_api.py $O/occ8k/run_results.db $O/host_api.txt > /dev/null; } && { [ -n "${KEEPDB:-}" ] || rm -f $O/occ8k/run_results.db; } ;;
+  abiso)
+    # A/B of knobs with the isolated pass (the kernels alone after the timed region): ENVS as envab, SHARDS
+    for n in ${SHARDS:-65536}; do for cfg in default ${ENVS:-}; do
+      envs=""; [ "$cfg" != default ] && envs=$(echo $cfg | tr ',' ' ')
+      env $envs timeout -k 10 240 python3 -u bench.py --no-cpu --no-configs --proofs $n --steps 30 > $O/abiso_${n}_$cfg.json 2> $O/abiso_${n}_$cfg.err || { echo "bench abiso $n $cfg failed"; tail -20 $O/abiso_${n}_$cfg.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/abiso_${n}_$cfg.json')); r=d['roofline']; print('$cfg shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s; iso', {k: round(v,3) for k,v in r['phase_ms'].items()})"
+    done; done ;;
+  afftest)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_affine.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/afftest.log 2>&1 || { echo "affine tests failed"; tail -60 $O/afftest.log; exit 1; }
+    tail -3 $O/afftest.log ;;
   benchcfg)
     # the driver's default command plus the side lines (config 2 / 4 / clean 4,096 / config 5, f3, f4, CPU legs)
     timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_full.json 2> $O/bench_full.err || { echo "bench full failed"; tail -30 $O/bench_full.err; exit 1; }
