@@ -14,17 +14,19 @@ per-proof statuses. The host->HBM input copies are outside the timed region; h2d
 reports them. Inputs: real mainnet proofs from the reference's fixtures,
 re-randomized on the GPU (synthetic, all valid; verified OK after the timed region).
 Batch scalars r_i come from the OS RNG inside the timed region (production mode).
-Batches in flight (--inflight; default 6): each GPU keeps that many
+Batches in flight (--inflight; default 6, 8 for shards of at most 8,192 proofs): each GPU keeps that many
 consecutive batches on the device, one context (buffers + streams) each. The host reads the
 oldest batch's partial and statuses and relaunches its context at once; the batch's verdict
-(gather + final exponentiation, on a checker context) runs on a worker thread in batch order
-(--sync-verdict: before the relaunch). Every batch is fully verified and its verdict is in
+runs off that loop: the exchange (gather) on a worker thread in batch order, the final
+exponentiation on one of --checkers verdict threads with a checker context each, so consecutive
+verdicts overlap (--sync-verdict: before the relaunch). Every batch is fully verified and its verdict is in
 inside the timed region (pipeline fill and drain included); a false verdict re-runs the batch
 with bisection. A batch's own latency is phase_ms.device_pipeline plus the final exponentiation.
 """
 import argparse
 import json
 import os
+import queue
 import sys
 import time
 
@@ -285,6 +287,8 @@ def main():
                     help="batches in flight per GPU, one context each (0: the default, 6)")
     ap.add_argument("--sync-verdict", action="store_true",
                     help="take each batch's verdict (gather + final exponentiation) before relaunching its context")
+    ap.add_argument("--checkers", type=int, default=2,
+                    help="verdict threads, one checker context each (final exponentiations of consecutive batches overlap)")
     ap.add_argument("--no-priority", action="store_true",
                     help="default-priority streams for the checker context and RCCL")
     ap.add_argument("--dist", action="store_true", help="use torch.distributed (RCCL) even at world size 1")
@@ -309,11 +313,16 @@ def main():
         # (65,536-proof shards, r02v: 2 -> 15.95, 3 -> 16.01, 4 -> 15.67, 5 -> 15.83 ms per batch; on the
         # round-4 kernels, 5 alternating repeats: 4 -> 14.02, 6 -> 13.78, 8 -> 13.91 mean ms per batch,
         # 6 the fastest in every repeat, profiles/r04y_inflight_64k.txt)
-        args.inflight = 6
+        # (round 6, profiles/r06m_depths.txt, one box: 8k shards 6 -> 2.60, 8 -> 2.40, 10 -> 2.53, 12 -> 2.98 ms
+        # per batch; 16k 6 -> 4.01, 8 -> 4.02; 32k 6 -> 6.80, 8 -> 6.90; 64k 6 -> 12.21, 8 -> 12.28)
+        args.inflight = 8 if (args.n + world - 1) // world <= 8192 else 6
     # two streams per context (main + side): give each its own hardware queue (set before the
     # HIP runtime starts; measured: 8k-proof shards 6 in flight 6.4 ms/batch on 4 queues, 5.0 on 12)
     # (RCCL's own streams want queues too: 8k shard over RCCL 5.58 ms/batch at 12 queues, 4.70 at 24)
-    hwq = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 24))
+    # (round 6) a stream pair per batch context (ZG_STREAM_PAIRS, the device pool: deeper pipelines than
+    # its default 8 would otherwise share pairs), two hardware queues per pair + the checkers' pairs
+    os.environ.setdefault("ZG_STREAM_PAIRS", str(min(16, max(8, args.inflight))))
+    hwq = min(32, max(int(os.environ.get("GPU_MAX_HW_QUEUES", "4")), 24, 2 * args.inflight + 8))
     if os.environ.get("ZG_BENCH_HWQ"):   # (tooling: an exact queue count for the sweeps in tools/gpu_r05.sh)
         hwq = min(32, int(os.environ["ZG_BENCH_HWQ"]))
     os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
@@ -342,7 +351,7 @@ def main():
     torch.cuda.set_device(local)
 
     from zebra_amd import Context
-    from zebra_amd.dist import combine_partials, run_pipelined, run_pipelined_deferred
+    from zebra_amd.dist import combine_partials, gather_partials, run_pipelined, run_pipelined_deferred
     src_proofs, src_kinds, idx, kinds, inputs, shard = workload(rank, world, args.n)
     ctx = Context(device=local, max_batch=shard)
     # batches in flight per GPU: each has its own context (buffers + streams); while the host
@@ -351,9 +360,15 @@ def main():
     # the verdicts (gather + final exponentiation) run on a checker context of their own, on a
     # worker thread in batch order, so a batch context is relaunched as soon as its partial and
     # statuses are read (zebra_amd.dist.run_pipelined_deferred)
-    checker = None if args.sync_verdict else Context(device=local, max_batch=64)
-    if checker and not args.no_priority:
-        checker.set_priority(True)
+    # (round 6) --checkers contexts, one per verdict thread: consecutive batches' final exponentiations
+    # overlap (zebra_amd.dist.run_pipelined_deferred gather / checks)
+    checkers = [] if args.sync_verdict else [Context(device=local, max_batch=64) for _ in range(max(1, args.checkers))]
+    for chk in checkers:
+        if not args.no_priority:
+            chk.set_priority(True)
+    free_checkers = queue.SimpleQueue()
+    for chk in checkers:
+        free_checkers.put(chk)
     t0 = time.perf_counter()
     proofs = ctx.synth_rerandomize(src_proofs, src_kinds, idx, 2 + 1000003 * rank)
     log("rank %d: generated %d re-randomized proofs in %.1f s" % (rank, shard, time.perf_counter() - t0))
@@ -399,9 +414,16 @@ def main():
         host.append((t1 - t0, 0.0, time.perf_counter() - t1))
         return part, sts
 
-    def verdict(part):
+    def gather(part):   # ordered stage: the exchange (RCCL all-gather at world > 1)
+        return gather_partials(part, world, rank, dev) if use_dist else [part]
+
+    def verdict(parts):  # pooled stage: ONE final exponentiation of the gathered partials' product
         t0 = time.perf_counter()
-        ok = check(part, checker)
+        chk = free_checkers.get()
+        try:
+            ok = chk.gt_check(parts)
+        finally:
+            free_checkers.put(chk)
         vtime.append(time.perf_counter() - t0)
         return ok
 
@@ -414,7 +436,8 @@ def main():
     def run(k):
         if args.sync_verdict:
             return run_pipelined(ctxs, k, launch, complete)
-        return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=lambda c: c.batch_ready())
+        return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=lambda c: c.batch_ready(),
+                                      gather=gather, checks=len(checkers))
 
     def barrier():
         if use_dist:
@@ -544,7 +567,8 @@ def main():
         "h2d_ms_per_batch": h2d,
         "host_ms_per_batch": {"launch": 1e3 * sum(ltime) / max(1, len(ltime)), "wait_partial": host_ms[0],
                               "exchange_and_final_exp": host_ms[1], "statuses": host_ms[2],
-                              "verdict": "sync" if args.sync_verdict else "deferred (worker thread, checker context)"},
+                              "verdict": "sync" if args.sync_verdict else
+                              "deferred (ordered gather thread, %d verdict threads with a checker context each)" % len(checkers)},
     }
     if rank == 0 and world == 1 and not args.no_configs:
         out["other_configs"] = other_configs(ctx, src_proofs, src_kinds, 0 if args.no_cpu else cpu_threads(args.cpu_threads))
@@ -590,7 +614,7 @@ def main():
     out["context_stats"] = st
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for c in ctxs + ([checker] if checker else []):
+    for c in ctxs + checkers:
         c.close()
     if use_dist:
         dist.destroy_process_group()

@@ -62,3 +62,42 @@ def test_without_ready_harvests_oldest_first():
     res = run_pipelined_deferred(ctxs, 9, launch, harvest, lambda p: True, lambda s: None)
     assert order == list(range(9))
     assert [sts for _, sts in res] == list(range(9))
+
+
+def test_gather_stage_ordered_checks_overlap():
+    """gather / checks (round 6): the exchange runs in batch order on one thread, the final
+    exponentiations on a pool -- two of them are in progress at once, results still in batch
+    order, false verdicts still re-verified."""
+    import threading
+    import time
+    ctxs = [FakeCtx(i, None) for i in range(3)]
+    seq = iter(range(100))
+    gathered, active, peak = [], [0], [0]
+    lock = threading.Lock()
+
+    def launch(c):
+        c.batch = next(seq)
+
+    def harvest(c):
+        return ("p", c.batch), c.batch
+
+    def gather(part):
+        gathered.append(part[1])
+        return [part, part]              # as if two ranks' partials
+
+    def verdict(parts):
+        assert len(parts) == 2
+        with lock:
+            active[0] += 1
+            peak[0] = max(peak[0], active[0])
+        time.sleep(0.02)
+        with lock:
+            active[0] -= 1
+        return parts[0][1] != 4
+
+    res = run_pipelined_deferred(ctxs, 10, launch, harvest, verdict, lambda s: ("redo", s),
+                                 gather=gather, checks=2)
+    assert gathered == list(range(10))
+    assert peak[0] == 2
+    assert [ok for ok, _ in res] == [s != 4 for s in range(10)]
+    assert res[4][1] == ("redo", 4) and res[5][1] == 5

@@ -187,5 +187,27 @@ for s in $STEPS; do
     # the driver's default command plus the side lines (config 2 / 4 / clean 4,096 / config 5, f3, f4, CPU legs)
     timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_full.json 2> $O/bench_full.err || { echo "bench full failed"; tail -30 $O/bench_full.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_full.json')); print(d['value'], d['ms_per_step']); oc=d['other_configs']; print({k: (round(v['ms_per_batch'],3) if isinstance(v, dict) and 'ms_per_batch' in v else v) for k, v in oc.items() if k != 'config5_replay'}); print(json.dumps(oc['config5_replay']))" ;;
+  ckab)
+    # verdict threads (bench.py --checkers) at 8k and 64k shards, and the K4 / latency-priority variants (isolated K4)
+    for n in ${SHARDS:-8192 65536}; do for ck in 1 2; do
+      timeout -k 10 240 python3 -u bench.py --no-cpu --no-configs --proofs $n --steps 40 --checkers $ck > $O/ck_${n}_$ck.json 2> $O/ck_${n}_$ck.err || { echo "bench ck $n $ck failed"; tail -20 $O/ck_${n}_$ck.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/ck_${n}_$ck.json')); print('checkers $ck shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), 'k4 iso', round(d['k4_msm_bucket_phase']['k4_total_ms'],3))"
+    done; done ;;
+  varab)
+    # library variants (ZG_LIB_VARIANT, tools/build_variant.py) against the default, in flight + isolated K4
+    for n in ${SHARDS:-8192 65536}; do for v in default $VARIANTS; do
+      lv=$v; [ $v = default ] && lv=
+      ZG_LIB_VARIANT=$lv timeout -k 10 240 python3 -u bench.py --no-cpu --no-configs --proofs $n --steps 40 > $O/var_${n}_$v.json 2> $O/var_${n}_$v.err || { echo "bench var $n $v failed"; tail -20 $O/var_${n}_$v.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/var_${n}_$v.json')); r=d['roofline']; print('$v shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), 'k4 iso', round(d['k4_msm_bucket_phase']['k4_total_ms'],3), 'iso', {k: round(v,3) for k,v in r['phase_ms'].items()})"
+    done; done ;;
+  depths)
+    # batches in flight by shard size: DEPTHS_<n>="6 8 ..." (default "6 8")
+    for n in ${SHARDS:-8192 65536}; do
+      eval ds=\${DEPTHS_$n:-"6 8"}
+      for inf in $ds; do
+        timeout -k 10 200 python3 -u bench.py --no-cpu --no-configs --no-iso --proofs $n --inflight $inf --steps 40 > $O/d_${n}_$inf.json 2> $O/d_${n}_$inf.err || { echo "bench depth $n $inf failed"; tail -20 $O/d_${n}_$inf.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/d_${n}_$inf.json')); print('shard $n inflight $inf', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s hwq', d['config']['hw_queues'])"
+      done
+    done ;;
   esac
 done

@@ -60,6 +60,26 @@ __global__ void __launch_bounds__(64) k_fe(const Fq12* in, Fq12* out, long long*
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+// the final exponentiation's single-lane pieces: the Fq12 inversion (coop_inv, lane 0) and a Frobenius
+__global__ void __launch_bounds__(64) k_inv(const Fq12* in, Fq12* out, long long* cyc) {
+  __shared__ CoopWS ws;
+  coop_init(&ws);
+  coop_load(&ws, 0, in[0]);
+  long long t0 = clock64();
+  coop_inv(&ws, 1, 0, 5);
+  long long t1 = clock64();
+  coop_frob(&ws, 2, 1, 2);
+  long long t2 = clock64();
+  coop_exp_by_x(&ws, 3, 2, BLS_X, 4);
+  long long t3 = clock64();
+  coop_store(&ws, 3, out[0]);
+  if (threadIdx.x == 0) {
+    cyc[0] = t1 - t0;
+    cyc[1] = t2 - t1;
+    cyc[2] = t3 - t2;
+  }
+}
+
 int main() {
   Fq12 h[2];
   uint32_t* w = (uint32_t*)h;
@@ -97,5 +117,9 @@ int main() {
   unsigned long long hsh = 0xcbf29ce484222325ull;
   for (size_t i = 0; i < sizeof(Fq12) / 4; i++) hsh = (hsh ^ ((const uint32_t*)o)[i]) * 0x100000001b3ull;
   printf("final_exp: %lld cycles, %.3f ms, output hash %016llx\n", c[0], ms, hsh);
+  hipLaunchKernelGGL(k_inv, dim3(1), dim3(64), 0, 0, din, dout, dc);
+  hipDeviceSynchronize();
+  hipMemcpy(c, dc, 24, hipMemcpyDeviceToHost);
+  printf("coop_inv %lld cycles, coop_frob %lld cycles, coop_exp_by_x %lld cycles\n", c[0], c[1], c[2]);
   return 0;
 }

@@ -48,6 +48,7 @@ using namespace zg;
 #define ZG_LINES_LANE_MIN 32768  // straight-line R-chain from here (r03: 64k 14.93 -> 14.47 ms per batch in
                                  // flight; 16k 4.90 -> 5.14 and 8k 3.21 -> 3.63 favour the staged program)
 #define ZG_DEFAULT_PAIRS 8       // stream pairs per device (ZG_STREAM_PAIRS overrides, 1..16)
+#define ZG_HI_PAIRS 4            // high-priority stream pairs per device (zg_set_priority round-robin)
 
 namespace zg {  // zg_merkle.hip
 struct MerkleDev;
@@ -89,7 +90,10 @@ struct zg_dev {
   std::mutex mu;  // the pool cursor and the VK cache
   int npairs = 0;
   hipStream_t main[16] = {}, side[16] = {};
-  hipStream_t hi_main = nullptr, hi_side = nullptr;  // high-priority pair (lazy, zg_set_priority)
+  // high-priority pairs (lazy, zg_set_priority): a few, so that concurrent checker contexts (one per
+  // verdict thread) do not serialise their final exponentiations on one stream
+  hipStream_t hi_main[ZG_HI_PAIRS] = {}, hi_side[ZG_HI_PAIRS] = {};
+  int hi_next = 0;
   int next = 0;
   struct VKEntry {
     RawVK raw;
@@ -182,6 +186,10 @@ struct zg_ctx {
   int quad_split = 1;        // ZG_QUAD_SPLIT: 1 a step's four lines multiply first, then into f (Q4IK + GM / GMSQ,
                              // round 6), 0 the fused Q4 / Q4SQ programs (same values)
   int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..8)
+  int pairs_late = 0;        // ZG_PAIRS_LATE=1: with group line products, the root's VK MSM + pairs go on the side
+                             // stream AFTER the group chains instead of before them (round 6, r06f: 8k with line
+                             // products 2.88 -> 2.77 ms per batch, still behind the quad chain's 2.61; 16k 4.19 ->
+                             // 4.30, 64k 12.33 -> 12.46: not the default)
   long k4_min = ZG_K4_MIN;   // ZG_K4_MIN overrides: K4 Pippenger from this many padded proofs, else decode GLV + C tree
   int k4_last = 1;           // the last batch summed r_i C_i with K4 (0: the C tree is built, bisection reuses it)
   int quads_last = 0;        // the last batch's f-chain ran four proofs per lane (no pair-level nodes)
@@ -244,8 +252,10 @@ static void dev_release(zg_dev* d) {
     if (d->main[i]) hipStreamDestroy(d->main[i]);
     if (d->side[i]) hipStreamDestroy(d->side[i]);
   }
-  if (d->hi_main) hipStreamDestroy(d->hi_main);
-  if (d->hi_side) hipStreamDestroy(d->hi_side);
+  for (int k = 0; k < ZG_HI_PAIRS; k++) {
+    if (d->hi_main[k]) hipStreamDestroy(d->hi_main[k]);
+    if (d->hi_side[k]) hipStreamDestroy(d->hi_side[k]);
+  }
   for (auto* e : d->vks) {
     if (e->d) hipFree(e->d);
     if (e->comb) hipFree(e->comb);
@@ -328,6 +338,7 @@ extern "C" zg_ctx* zg_create(const zg_config* cfg) {
   if (const char* e = getenv("ZG_LINES_AFFINE_XL")) ctx->lines_affine_xl = atoi(e) ? 1 : 0;
   if (ctx->lines_affine_xl) ctx->lines_affine = 4;
   if (const char* e = getenv("ZG_LINE_PROD_PARTS")) ctx->lp_parts = std::max(1, std::min(ZG_LP_PARTS_MAX, atoi(e)));
+  if (const char* e = getenv("ZG_PAIRS_LATE")) ctx->pairs_late = atoi(e) ? 1 : 0;
   if (ctx->line_group != -1 && (ctx->line_group < 4 || (ctx->line_group & (ctx->line_group - 1)))) ctx->line_group = 0;
   if (const char* e = getenv("ZG_K4_MIN")) ctx->k4_min = atol(e);
   if (const char* e = getenv("ZG_FCHAIN_SINGLE")) ctx->singles = atoi(e);
@@ -823,21 +834,20 @@ static int run_pipeline(zg_ctx* ctx) {
   NodeBufs nb = {nullptr, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, 1};
   ctx->alone_last = alone;
   // side stream: K4 + the root's VK-side work (or, serial_side, on the main stream after the tree)
-  auto side_work = [&](hipStream_t st) -> int {
+  auto side_k4 = [&](hipStream_t st) -> int {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     HIPCHK(launch_msm_root(st, b, ctx->msm, nullptr, ctx->ev[8], ctx->ev[9], k4, alone));
     if (!k4) HIPCHK(launch_c_tree(ctx, b, st, nullptr));
     HIPCHK(hipEventRecord(ctx->ev[10], st));
+    return ZG_OK;
+  };
+  auto side_pairs = [&](hipStream_t st) -> int {
     int r = launch_node_msm_pairs(ctx, b, nb, st);
     if (r) return r;
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     return ZG_OK;
   };
   int rc;
-  if (!ctx->serial_side) {
-    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
-    if ((rc = side_work(ctx->side))) return rc;
-  }
   // main stream: the R-chain (lines; also the G2 subgroup checks of the B_i), then the f-chain
   // two proofs per lane: the f-chain writes the tree level of proof pairs (npad/2 nodes)
   const unsigned groups = (unsigned)((ctx->npad + 63) / 64);
@@ -873,6 +883,15 @@ static int run_pipeline(zg_ctx* ctx) {
   // program reads its (a, b) lines; bisection re-forms projective lines for the chains below the groups
   const bool affine = lineprod && ctx->lines_affine;
   ctx->affine_last = affine;
+  // the group chains run on the side stream in parts (below): with pairs_late the root's VK MSM + pairs
+  // follow the last chain part there instead of preceding the first (8k with line products, r05aa: the
+  // first chain waited 2.8 ms behind k_node_pairs although its part was formed)
+  const bool late = lineprod && ctx->lp_parts > 1 && ctx->pairs_late && !ctx->serial_side;
+  if (!ctx->serial_side) {
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
+    if ((rc = side_k4(ctx->side))) return rc;
+    if (!late && (rc = side_pairs(ctx->side))) return rc;
+  }
   if (fused) {  // one launch, f-chain blocks consuming each published lines step (k_lines_fchain)
     HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_prog, 0, groups * sizeof(int), ctx->stream));
@@ -921,6 +940,7 @@ static int run_pipeline(zg_ctx* ctx) {
         }
         HIPCHK(hipEventRecord(ctx->ev[14 + ZG_LP_PARTS_MAX], ctx->side));
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[14 + ZG_LP_PARTS_MAX], 0));
+        if (late && (rc = side_pairs(ctx->side))) return rc;  // beside the product tree on the main stream
       }
     } else if (quads) {
       HIPCHK(launch_prog_fchain4(qgroups, ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->quad_split));
@@ -933,7 +953,7 @@ static int run_pipeline(zg_ctx* ctx) {
   HIPCHK(launch_f_tree(ctx, b, lineprod ? ctx->npad / gsize : ctx->npad / (singles ? 1 : quads ? 4 : 2)));
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   if (ctx->serial_side) {
-    if ((rc = side_work(ctx->stream))) return rc;
+    if ((rc = side_k4(ctx->stream)) || (rc = side_pairs(ctx->stream))) return rc;
   } else {
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev[6], 0));  // side-stream K4 + root pairs complete
   }
@@ -1224,14 +1244,15 @@ extern "C" int zg_set_priority(zg_ctx* ctx, int high) {
   zg_dev* d = ctx->dev;
   if (high) {
     std::lock_guard<std::mutex> gd(d->mu);
-    if (!d->hi_main) {
+    const int k = d->hi_next++ % ZG_HI_PAIRS;
+    if (!d->hi_main[k]) {
       int lo = 0, hi = 0;
       HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));  // numerically lower = higher priority
-      HIPCHK(hipStreamCreateWithPriority(&d->hi_main, hipStreamNonBlocking, hi));
-      HIPCHK(hipStreamCreateWithPriority(&d->hi_side, hipStreamNonBlocking, hi));
+      HIPCHK(hipStreamCreateWithPriority(&d->hi_main[k], hipStreamNonBlocking, hi));
+      HIPCHK(hipStreamCreateWithPriority(&d->hi_side[k], hipStreamNonBlocking, hi));
     }
-    ctx->stream = d->hi_main;
-    ctx->side = d->hi_side;
+    ctx->stream = d->hi_main[k];
+    ctx->side = d->hi_side[k];
   } else {
     ctx->stream = d->main[ctx->pair];
     ctx->side = d->side[ctx->pair];

@@ -274,29 +274,45 @@ __device__ void coop_frob(CoopWS* ws, int dst, int a, int k) {
   __syncthreads();
 }
 
-// slot[dst] = slot[a]^-1 (one lane: the tower inversion is a few Fq2 products + one Fq inverse)
-__device__ void coop_inv(CoopWS* ws, int dst, int a) {
+// slot[dst] = slot[a]^-1 through the norm to Fq6 (round 6: the tower arithmetic off lane 0 -- on one lane
+// it was four Fq6 and twelve Fq2 products in sequence, ~0.35 ms of the final exponentiation's ~1.7):
+//   g = f conj(f) = f0^2 - v f1^2 in Fq6 (coop_mul), then the Fq6 inverse of g on lanes 0..5 (its six,
+//   then three, then three Fq2 products in parallel), the Fq2 norm's Fq inverse on lane 0 (zg_bingcd.h),
+//   and f^-1 = conj(f) g^-1 (coop_mul). Uses slot tmp (!= dst, a) and the op workspace v.
+__device__ void coop_inv(CoopWS* ws, int dst, int a, int tmp) {
   const int lane = threadIdx.x & 63;
-  if (lane == 0) {
-    Fq12 f;
-    Fq2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-    for (int j = 0; j < 6; j++) *c[j] = coop_get2(ws, a, j);
-    Fq6 t = f6_sub(f6_mul(f.c0, f.c0), f6_mul_nr(f6_mul(f.c1, f.c1)));
-    Fq2 c0 = f2_sub(f2_sqr(t.c0), f2_mul_nr(f2_mul(t.c1, t.c2)));
-    Fq2 c1 = f2_sub(f2_mul_nr(f2_sqr(t.c2)), f2_mul(t.c0, t.c1));
-    Fq2 c2 = f2_sub(f2_sqr(t.c1), f2_mul(t.c0, t.c2));
-    Fq2 n = f2_add(f2_mul(t.c0, c0), f2_mul_nr(f2_add(f2_mul(t.c2, c1), f2_mul(t.c1, c2))));
-    Fq ni = fq_inv(fq_add(fq_sqr(n.c0), fq_sqr(n.c1)));
-    Fq2 nin = {fq_mul(n.c0, ni), fq_neg(fq_mul(n.c1, ni))};
-    Fq6 ti = {f2_mul(c0, nin), f2_mul(c1, nin), f2_mul(c2, nin)};
-    Fq12 r = {f6_mul(f.c0, ti), f6_neg(f6_mul(f.c1, ti))};
-    Fq2* o[6] = {&r.c0.c0, &r.c0.c1, &r.c0.c2, &r.c1.c0, &r.c1.c1, &r.c1.c2};
-    for (int j = 0; j < 6; j++) {
-      ws->slot[dst][2 * j] = o[j]->c0;
-      ws->slot[dst][2 * j + 1] = o[j]->c1;
-    }
+  coop_conj(ws, tmp, a);
+  coop_mul(ws, dst, a, tmp);  // g: coefficients 0..5 = (t0, t1, t2), 6..11 = 0
+  Fq2* x = reinterpret_cast<Fq2*>(&ws->v[24]);  // exchange: x[0..5] products, x[6..8] c, x[9..11] q, x[12] nin
+  if (lane < 6) {  // t0^2, t1 t2, t2^2, t0 t1, t1^2, t0 t2
+    const int i = lane == 0 || lane == 3 || lane == 5 ? 0 : lane == 1 || lane == 4 ? 1 : 2;
+    const int j = lane == 0 ? 0 : lane == 1 || lane == 2 ? 2 : lane == 3 || lane == 4 ? 1 : 2;
+    x[lane] = f2_mul(coop_get2(ws, dst, i), coop_get2(ws, dst, j));
   }
   __syncthreads();
+  if (lane < 3) {  // c0 = t0^2 - xi t1 t2, c1 = xi t2^2 - t0 t1, c2 = t1^2 - t0 t2
+    const Fq2 u = x[2 * lane], w = x[2 * lane + 1];
+    x[6 + lane] = lane == 0 ? f2_sub(u, f2_mul_nr(w)) : lane == 1 ? f2_sub(f2_mul_nr(u), w) : f2_sub(u, w);
+  }
+  __syncthreads();
+  if (lane < 3)  // q = t0 c0, t2 c1, t1 c2
+    x[9 + lane] = f2_mul(coop_get2(ws, dst, lane == 0 ? 0 : lane == 1 ? 2 : 1), x[6 + lane]);
+  __syncthreads();
+  if (lane == 0) {  // n = q0 + xi (q1 + q2); n^-1 = conj(n) / (n0^2 + n1^2)
+    const Fq2 n = f2_add(x[9], f2_mul_nr(f2_add(x[10], x[11])));
+    const Fq ni = fq_inv(fq_add(fq_sqr(n.c0), fq_sqr(n.c1)));
+    x[12] = {fq_mul(n.c0, ni), fq_neg(fq_mul(n.c1, ni))};
+  }
+  __syncthreads();
+  Fq2 gi;
+  if (lane < 3) gi = f2_mul(x[6 + lane], x[12]);
+  __syncthreads();
+  if (lane < 6) {  // g^-1 = (c0, c1, c2) n^-1 as an Fq12 with a zero w part
+    ws->slot[dst][2 * lane] = lane < 3 ? gi.c0 : fp_zero<FqM>();
+    ws->slot[dst][2 * lane + 1] = lane < 3 ? gi.c1 : fp_zero<FqM>();
+  }
+  __syncthreads();
+  coop_mul(ws, dst, tmp, dst);
 }
 
 // slot[dst] = conj(slot[a]^x)  (exp_by_x of the pairing chain; a cyclotomic)
@@ -317,7 +333,7 @@ __device__ void coop_final_exp(CoopWS* ws, int in, int out) {
   enum { F = 0, Rr = 1, Y0 = 2, Y1 = 3, Y2 = 4, Y3 = 5, T = 6, F2 = 7 };
   if (in != F) coop_copy(ws, F, in);
   coop_conj(ws, Rr, F);         // f1 = conj(f)
-  coop_inv(ws, F2, F);          // f2 = f^-1
+  coop_inv(ws, F2, F, T);       // f2 = f^-1
   coop_mul(ws, Rr, Rr, F2);     // r = f1 * f2
   coop_copy(ws, F2, Rr);        // f2 = r
   coop_frob(ws, Rr, Rr, 2);

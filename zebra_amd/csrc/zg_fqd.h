@@ -240,6 +240,46 @@ ZG_INL G1D g1d_dbl(const G1D& p) {
   return {X3, Y3, Z3};
 }
 
+// g1d_dbl on a whole wave for a lone doubling chain (K4's top-window scaling, zg_msm.hip): the same
+// formulas and bounds, so the same digits, with the seven products of dbl-2009-l in three levels of
+// independent products, one per lane (lanes 0..2), exchanged through `xch` (3 FqD of LDS, the wave's
+// own): {A = X^2, B = Y^2, YZ}, {C = B^2, T = (X + B)^2, F = (3A)^2}, {E (D - X3)}. Every lane of the
+// wave calls it with the same p and gets the result.
+ZG_INL FqD fqd_pick3(int k, const FqD& a, const FqD& b, const FqD& c) {
+  FqD r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.d[i] = k == 0 ? a.d[i] : k == 1 ? b.d[i] : c.d[i];
+  return r;
+}
+ZG_INL void fqd_xch_put(FqD* xch, int lane, const FqD& v) {
+  if (lane < 3) xch[lane] = v;
+  __syncthreads();
+}
+ZG_INL G1D g1d_dbl_wave(const G1D& p, FqD* xch) {
+  const int lane = threadIdx.x & 63, k = lane < 3 ? lane : 0;
+  // level 1: A = X X, B = Y Y, YZ = Y Z
+  const FqD m1 = fqd_mul(fqd_pick3(k, p.x, p.y, p.y), fqd_pick3(k, p.x, p.y, p.z));
+  fqd_xch_put(xch, lane, m1);
+  const FqD A = xch[0], B = xch[1], YZ = xch[2];
+  __syncthreads();
+  // level 2: C = B^2, T = (X + B)^2, F = E^2 with E = 3 A
+  const FqD E = fqd_smul<3>(A);
+  const FqD m2 = fqd_sqr(fqd_pick3(k, B, fqd_add(p.x, B), E));
+  fqd_xch_put(xch, lane, m2);
+  const FqD C = xch[0], T = xch[1], F = xch[2];
+  __syncthreads();
+  const FqD D = fqd_smul<2>(fqd_sub2<5>(T, A, C));
+  const FqD X3 = fqd_sub<29, 1, 2>(F, D);
+  // level 3: E (D - X3)
+  const FqD m3 = fqd_mul(E, fqd_sub<32, 1, 1>(D, X3));
+  fqd_xch_put(xch, lane, m3);
+  const FqD Y3a = xch[0];
+  __syncthreads();
+  const FqD Y3 = fqd_sub<17, 1, 1>(Y3a, fqd_smul<8>(C));
+  const FqD Z3 = fqd_smul<2>(YZ);
+  return {X3, Y3, Z3};
+}
+
 // madd-2007-bl with complete case handling: p + q for q affine and finite, qx < 2p, qy < 4p.
 // In: the invariant. Out: X < 9p, Y < 7p, Z < 4p (or g1d_dbl's, or q itself). 11 products.
 ZG_INL G1D g1d_add_aff(const G1D& p, const FqD& qx, const FqD& qy) {

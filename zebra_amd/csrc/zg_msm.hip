@@ -11,6 +11,10 @@
 #include "../../include/zg.h"
 #include "zg_msm.h"
 
+#ifndef ZG_K4_DBL_WAVE
+#define ZG_K4_DBL_WAVE 1  // k_msm_group's window doublings on three lanes (g1d_dbl_wave, round 6)
+#endif
+
 namespace zg {
 
 // the scalar of point j of proof i: j = 0 -> k0 = 2a + 1 (65 bits), j = 1 -> k1 = b
@@ -255,12 +259,23 @@ __global__ void __launch_bounds__(64) k_msm_group(MsmBufs m, const int* gate) {
     sh[s] = u;
     __syncthreads();
   }
-  if (s == 0) {  // 2^shift(w) W_w: this window's part of sum_w 2^shift(w) W_w
+  // 2^shift(w) W_w: this window's part of sum_w 2^shift(w) W_w, the kernel's critical path (the top
+  // window: 55 doublings at 64k). ZG_K4_DBL_WAVE (default): each doubling's seven products as three
+  // levels over lanes 0..2 (g1d_dbl_wave, same digits); 0: the doublings on lane 0 alone.
+  // Infinity (Z = 0) stays infinity.
+  const int w = g % S.w;
+#if ZG_K4_DBL_WAVE
+  __shared__ FqD xch[3];
+  G1D q = sh[0];
+  for (int k = 0; k < S.shift(w); k++) q = g1d_dbl_wave(q, xch);
+  if (s == 0) m.wsum[g] = q;
+#else
+  if (s == 0) {
     G1D q = sh[0];
-    const int w = g % S.w;
-    for (int k = 0; k < S.shift(w); k++) q = g1d_dbl(q);  // infinity (Z = 0) stays infinity
+    for (int k = 0; k < S.shift(w); k++) q = g1d_dbl(q);
     m.wsum[g] = q;
   }
+#endif
 }
 
 // per key: sum_w of the scaled window sums (k_msm_group) -> the root node of the C-sum tree (node 1)

@@ -44,6 +44,13 @@ def combine_partials(partial, check, world, rank, device):
     `partial` is one 576-B partial, or a list of k of them when a rank verifies k shards of the
     batch (every rank must pass the same k): the gather then moves world x k partials in the
     same single collective, ordered rank-major (rank 0's k shards first)."""
+    return check(gather_partials(partial, world, rank, device))
+
+
+def gather_partials(partial, world, rank, device):
+    """The exchange step of combine_partials alone: every rank's partial(s), rank-major, as a list
+    of 576-B bytes (same on every rank). Calls must not overlap and must run in the same order on
+    every rank (run_pipelined_deferred's ordered gather stage)."""
     import contextlib
     import numpy as np
     import torch
@@ -60,7 +67,7 @@ def combine_partials(partial, check, world, rank, device):
     if stream is not None:
         stream.synchronize()
     allb = back.numpy().tobytes()
-    return check([allb[GT_BYTES * j:GT_BYTES * (j + 1)] for j in range(world * k)])
+    return [allb[GT_BYTES * j:GT_BYTES * (j + 1)] for j in range(world * k)]
 
 
 def run_pipelined(ctxs, k, launch, complete):
@@ -80,7 +87,7 @@ def run_pipelined(ctxs, k, launch, complete):
     return out
 
 
-def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None):
+def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None, gather=None, checks=1):
     """run_pipelined with the verdict taken off the context's critical path.
 
     harvest(ctx) -> (partial, statuses) waits for a batch's Miller partial and reads its
@@ -95,12 +102,27 @@ def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None):
     run_pipelined. A batch whose verdict is false is re-verified by redo(batch_index) -> statuses
     (bisection on a fresh pass: per-proof results do not depend on the batch scalars) after the
     pipeline has drained. Returns the k (verdict, statuses) pairs in batch order; all verdicts are
-    in before it returns."""
+    in before it returns.
+
+    gather / checks (round 6): with gather(partial) -> partials given, the worker thread runs only
+    that exchange (the collective) in batch order and hands verdict(partials) -- the final
+    exponentiation, a lone wave on the device for ~2 ms -- to a pool of `checks` threads, so the
+    verdicts of consecutive batches overlap instead of bounding the batch rate (8k shards, 6 in
+    flight: one verdict thread was busy 2.16 of every 2.61 ms). verdict must then be thread-safe
+    (e.g. one checker context per thread)."""
     import time
     from concurrent.futures import ThreadPoolExecutor
     free, inflight = list(ctxs), []   # inflight: (batch index, ctx) in launch order
     done, res = {}, {}                # harvested, verdict not yet submitted / submitted
     nxt = launched = 0
+    pool = ThreadPoolExecutor(max_workers=max(1, checks)) if gather is not None else None
+
+    def staged(part):                 # ordered worker: the exchange, then the check on the pool
+        return pool.submit(verdict, gather(part))
+
+    def result(f):
+        r = f.result()
+        return r.result() if pool is not None else r
     with ThreadPoolExecutor(max_workers=1) as ex:
         while launched < k or inflight:
             while free and launched < k:
@@ -119,7 +141,9 @@ def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None):
             free.append(c)
             while nxt in done:         # verdicts (collectives) strictly in batch order
                 part, sts = done.pop(nxt)
-                res[nxt] = (sts, ex.submit(verdict, part))
+                res[nxt] = (sts, ex.submit(staged if pool is not None else verdict, part))
                 nxt += 1
-        oks = [res[s][1].result() for s in range(k)]
+        oks = [result(res[s][1]) for s in range(k)]
+    if pool is not None:
+        pool.shutdown()
     return [(ok, res[s][0] if ok else redo(s)) for s, ok in enumerate(oks)]
