@@ -119,6 +119,7 @@ def _ctx_env(env, n):
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_LINE_PROD_PARTS": 1},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_LINE_PROD_PARTS": 3},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 32, "ZG_SERIAL_SIDE": 1},
+                                 {"ZG_LINES_FCHAIN": 0, "ZG_FCHAIN_QUADS": 1, "ZG_LINE_GROUP": 4, "ZG_PAIRS_LATE": 1},
                                  {"ZG_LINES_FCHAIN": 0, "ZG_LINES_LANE": 1}, {"ZG_K4_MIN": 1}],
                          ids=lambda e: ",".join("%s=%s" % kv for kv in e.items()))
 def test_context_knobs_give_the_same_partial(work4k, env):

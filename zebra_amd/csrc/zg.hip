@@ -185,7 +185,8 @@ struct zg_ctx {
   int affine_last = 0;       // the last batch's lines are affine (bisection re-forms projective ones)
   int quad_split = 1;        // ZG_QUAD_SPLIT: 1 a step's four lines multiply first, then into f (Q4IK + GM / GMSQ,
                              // round 6), 0 the fused Q4 / Q4SQ programs (same values)
-  int lp_parts = 4;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains (1..8)
+  int lp_parts = 0;          // ZG_LINE_PROD_PARTS: step parts overlapping line products and chains: 1..8 equal
+                             // parts, 0 (default) wave-aligned parts (lineprod_parts)
   int pairs_late = 0;        // ZG_PAIRS_LATE=1: with group line products, the root's VK MSM + pairs go on the side
                              // stream AFTER the group chains instead of before them (round 6, r06f: 8k with line
                              // products 2.88 -> 2.77 ms per batch, still behind the quad chain's 2.61; 16k 4.19 ->
@@ -811,6 +812,30 @@ static hipError_t launch_f_tree(zg_ctx* ctx, const BatchBufs& b, size_t top) {
   }
   return hipSuccess;
 }
+// The step parts of the group line products (k_line_prod over steps [n0, n1) while the side stream
+// runs the chains of the part before). A launch holds (n1 - n0) x ceil(m / 64) blocks of one CU each
+// (153.6 KB of LDS), so a part whose block count is not a multiple of the CU count ends in a partial
+// wave of blocks: 64k with four equal parts of 17 steps was 544 blocks = 2.125 block waves in 3.
+// wave-aligned (req = 0): parts of two full block waves, the remainder last -- a short last part whose
+// chain (the exposed tail) is short too. From the second part on, the previous part's chains hold
+// ceil(m / 64) CUs of their own (same block shape), so a wave there has ncu - that many CUs: 64k, 2,048
+// groups, 32 blocks a step: steps [0, 16), then 14-step parts, [58, 68) last. req >= 1: req equal parts.
+static int lineprod_parts(int req, int m, int ncu, int* bounds) {
+  int parts = req;
+  if (req <= 0) {
+    const int bps = (m + 63) / 64;
+    const int first = 2 * std::max(1, ncu / bps), spw = std::max(1, (ncu - bps) / bps);
+    int len = 2 * spw;
+    while (1 + (ZG_NCOEFF - std::min(first, ZG_NCOEFF) + len - 1) / len > ZG_LP_PARTS_MAX) len += spw;
+    parts = 0;
+    for (int n = 0; n < ZG_NCOEFF; n += parts == 1 ? first : len) bounds[parts++] = n;
+    bounds[parts] = ZG_NCOEFF;
+    return parts;
+  }
+  for (int k = 0; k <= parts; k++) bounds[k] = ZG_NCOEFF * k / parts;
+  return parts;
+}
+
 static int run_pipeline(zg_ctx* ctx) {
   BatchBufs b = batch_bufs(ctx);
   ctx->eager = 0;
@@ -886,7 +911,7 @@ static int run_pipeline(zg_ctx* ctx) {
   // the group chains run on the side stream in parts (below): with pairs_late the root's VK MSM + pairs
   // follow the last chain part there instead of preceding the first (8k with line products, r05aa: the
   // first chain waited 2.8 ms behind k_node_pairs although its part was formed)
-  const bool late = lineprod && ctx->lp_parts > 1 && ctx->pairs_late && !ctx->serial_side;
+  const bool late = lineprod && ctx->lp_parts != 1 && ctx->pairs_late && !ctx->serial_side;
   if (!ctx->serial_side) {
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev[1], 0));
     if ((rc = side_k4(ctx->side))) return rc;
@@ -924,14 +949,16 @@ static int run_pipeline(zg_ctx* ctx) {
       // in parts of the 68 steps: the side stream (its K4 / VK work long done by then) runs the
       // chains over part k while the main stream forms part k + 1, so the chains' latency hides
       // behind the line products except for the last part
-      const int m = (int)(ctx->npad / gsize), parts = ctx->lp_parts;
+      const int m = (int)(ctx->npad / gsize);
+      int bounds[ZG_LP_PARTS_MAX + 1];
+      const int parts = lineprod_parts(ctx->lp_parts, m, ctx->ncu, bounds);
       if (parts <= 1) {
         HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, 0, ZG_NCOEFF,
                                           ctx->quad_split, affine));
         HIPCHK(launch_prog_fchaing(ctx->stream, b, (const Fq2*)ctx->d_lprod, ctx->d_fstate, m, 0, ZG_NCOEFF));
       } else {
         for (int k = 0; k < parts; k++) {
-          const int n0 = ZG_NCOEFF * k / parts, n1 = ZG_NCOEFF * (k + 1) / parts;
+          const int n0 = bounds[k], n1 = bounds[k + 1];
           HIPCHK(launch_prog_lineprod(ctx->stream, b, (const Fq2*)ctx->d_lines, ctx->d_lprod, gsize, n0, n1,
                                             ctx->quad_split, affine));
           HIPCHK(hipEventRecord(ctx->ev[14 + k], ctx->stream));
