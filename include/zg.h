@@ -191,6 +191,27 @@ int zg_prep_joinsplit_bn(const uint8_t anchor[32], const uint8_t random_seed[32]
 int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32], const uint8_t pubkey[32],
             uint8_t out[32]);
 
+/* ---- the same preparation for a whole import window in ONE call (round 6): the Sapling
+ * descriptions on the GPU (one lane each: both Jubjub decodes and small-order checks, the field
+ * checks, multipacking -- the per-description work of zg_prep_spend / zg_prep_output), the
+ * JoinSplits on host threads meanwhile (BLAKE2b hSig and bit packing, as zg_prep_joinsplit[_bn]).
+ * The caller side of accept_chain.rs:76-81 (rayon over a block's transactions) feeds it a block or
+ * window at once. kinds[i] ZG_PREP_KIND_*; fields n x ZG_PREP_FIELD_BYTES per kind:
+ *   SPEND        cv | anchor | nullifier | rk                                     (4 x 32 B)
+ *   OUTPUT       cv | cmu | epk                                                   (3 x 32 B)
+ *   JOINSPLIT[_BN] anchor | random_seed | nf0 | nf1 | mac0 | mac1 | cm0 | cm1 | pubkey (9 x 32 B)
+ *                | vpub_old | vpub_new                                          (2 x 8 B LE)
+ * -> inputs n x 288 B (the rows of zg_verify_batch / zg_pghr13_verify: 7 / 5 / 9 x 32 B, zero
+ * padded), codes n x ZG_PREP_* (the single-description functions' return values, same order of
+ * checks). Returns ZG_OK or an error code. */
+#define ZG_PREP_KIND_SPEND 0
+#define ZG_PREP_KIND_OUTPUT 1
+#define ZG_PREP_KIND_JOINSPLIT 2
+#define ZG_PREP_KIND_JOINSPLIT_BN 3
+#define ZG_PREP_FIELD_BYTES 304
+int zg_prep_batch(zg_ctx* ctx, size_t n, const uint8_t* kinds, const uint8_t* fields, uint8_t* inputs,
+                  uint8_t* codes);
+
 /* ---- Sapling signatures and Jubjub points on the GPU: the checks that sit
  * next to the Groth16 proofs in accept_sapling, batched. Any n; device memory per call.
  *   zg_redjubjub_verify <- redjubjub::PublicKey::read + verify (sapling-crypto @21084bde), called at

@@ -42,6 +42,12 @@ pub const ZG_E_STATE: c_int = -6;
 pub const ZG_E_TREE_FULL: c_int = -7;
 pub const ZG_E_DEBUG: c_int = -8;
 
+pub const ZG_PREP_KIND_SPEND: u8 = 0;
+pub const ZG_PREP_KIND_OUTPUT: u8 = 1;
+pub const ZG_PREP_KIND_JOINSPLIT: u8 = 2;
+pub const ZG_PREP_KIND_JOINSPLIT_BN: u8 = 3;
+pub const ZG_PREP_FIELD_BYTES: usize = 304;
+
 pub const ZG_PROOF_BYTES: usize = 192;
 pub const ZG_FR_BYTES: usize = 32;
 pub const ZG_MAX_INPUTS: usize = 9;
@@ -105,6 +111,8 @@ extern "C" {
                                 commitments: *const u8, vpub_old: u64, vpub_new: u64, pubkey: *const u8,
                                 inputs: *mut u8) -> c_int;
     pub fn zg_hsig(random_seed: *const u8, nf0: *const u8, nf1: *const u8, pubkey: *const u8, out: *mut u8) -> c_int;
+    pub fn zg_prep_batch(ctx: *mut ZgCtx, n: usize, kinds: *const u8, fields: *const u8, inputs: *mut u8,
+                         codes: *mut u8) -> c_int;
 
     pub fn zg_redjubjub_verify(ctx: *mut ZgCtx, n: usize, vk: *const u8, sig: *const u8, msg: *const u8,
                                gen: *const u8, ok: *mut u8) -> c_int;

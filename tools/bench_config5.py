@@ -13,7 +13,10 @@ re-randomized on the GPU per block, Sprout-Groth16 : Sapling = 1 : 4 by proof co
   * the oracle's C++ bellman restatement (oracle/cpu/bellman_cpu.cpp, checker / CPU baseline only)
     through the same collector on the same blocks, on the job's CPU threads.
 
-The product has no CPU path: a small block goes to the GPU like any other.
+Every proof goes to the GPU, whatever the block size (the product has no CPU verification path,
+DESIGN.md §5). The public-input preparation of a window from 64 descriptions runs as one
+zg_prep_batch call (Sapling descriptions on the GPU), below that on the host functions, as the
+reference prepares them on the host (collector._GPU_PREP_MIN).
 """
 import json
 import os

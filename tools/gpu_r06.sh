@@ -209,5 +209,11 @@ for s in $STEPS; do
         python3 -c "import json; d=json.load(open('$O/d_${n}_$inf.json')); print('shard $n inflight $inf', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s hwq', d['config']['hw_queues'])"
       done
     done ;;
+  preptest)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_prep_batch.py tests/test_collector.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/preptest.log 2>&1 || { echo "prep tests failed"; tail -60 $O/preptest.log; exit 1; }
+    tail -3 $O/preptest.log ;;
+  config5)
+    timeout -k 10 300 python3 -u tools/run_config5.py ${C5ARGS:-} > $O/config5.json 2> $O/config5.err || { echo "config5 failed"; tail -30 $O/config5.err; exit 1; }
+    cat $O/config5.json ;;
   esac
 done

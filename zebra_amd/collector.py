@@ -19,8 +19,10 @@ reference's:
 
 The checks that are not proofs or Sapling signatures (JoinSplit ed25519 signature, tree
 roots, nullifiers, the transparent checks before the shielded stages) are evaluated by the
-caller exactly as today and handed in as outcomes; the collector prepares every Groth16 public
-input with the product's host code (zg_prep_*), verifies all Groth16 proofs of the window in
+caller exactly as today and handed in as outcomes; the collector prepares every public input of
+the window in one zg_prep_batch call (the Sapling descriptions' Jubjub decodes on the GPU, the
+JoinSplits on host threads; without a context, the per-description zg_prep_* host functions),
+verifies all Groth16 proofs of the window in
 one zg_verify_batch call and all PGHR13 proofs of pre-Sapling JoinSplits (sprout.rs:61-67,
 inputs Input::into_bn_frs via zg_prep_joinsplit_bn) in one zg_pghr13_verify call, and
 re-injects the per-proof statuses in reference order: a PHGR description that fails to decode
@@ -92,6 +94,11 @@ class Tx:
 
 _POOL = None
 _PAR_MIN = 32   # prep jobs below this run inline (a pool round trip costs more than they do)
+# windows from this many descriptions go through zg_prep_batch (the GPU); below, the host functions:
+# a lone 9-description block took 6.6 ms with host prep and 8.6 ms with the batched call (its copies
+# and launch), a 401-description block 12.1 -> 9.8 ms, a 9,609-description window 383 -> 35 ms
+# (tools/bench_config5.py; profiles/r06q_config5.txt)
+_GPU_PREP_MIN = 64
 
 
 def _prep_pool():
@@ -123,28 +130,51 @@ def _run_prep(job):
         return e
 
 
-def _queue(txs):
-    """prepare inputs; returns (Groth16 items, PGHR13 items, per-tx plans). A plan entry refers
-    to a queued proof by index ("proof" / "pghr"), or carries a prep error or a caller verdict.
-    The prep calls of the whole window run first (in parallel for a large window), then the
-    items and plans are assembled in reference order."""
+def _jobs(txs):
+    """the window's preparation jobs in reference order: (PREP_KIND_*, arguments of the prep function)"""
     jobs = []
     for tx in txs:
         for d in tx.joinsplits:
             if tx.js_pubkey is None or (not d.groth and d.pghr_ok is not None):
                 continue
-            fn = zg.prep_joinsplit if d.groth else zg.prep_joinsplit_bn
-            jobs.append((fn, (d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old, d.vpub_new,
-                              tx.js_pubkey)))
+            jobs.append((zg.PREP_KIND_JOINSPLIT if d.groth else zg.PREP_KIND_JOINSPLIT_BN,
+                         (d.anchor, d.random_seed, d.nullifiers, d.macs, d.commitments, d.vpub_old, d.vpub_new,
+                          tx.js_pubkey)))
         for s in tx.spends:
-            jobs.append((zg.prep_spend, (s.cv, s.anchor, s.nullifier, s.rk)))
+            jobs.append((zg.PREP_KIND_SPEND, (s.cv, s.anchor, s.nullifier, s.rk)))
         for o in tx.outputs:
-            jobs.append((zg.prep_output, (o.cv, o.cmu, o.epk)))
-    if len(jobs) >= _PAR_MIN:
-        done = list(_prep_pool().map(_run_prep, jobs, chunksize=16))
+            jobs.append((zg.PREP_KIND_OUTPUT, (o.cv, o.cmu, o.epk)))
+    return jobs
+
+
+_PREP_FN = {zg.PREP_KIND_SPEND: zg.prep_spend, zg.PREP_KIND_OUTPUT: zg.prep_output,
+            zg.PREP_KIND_JOINSPLIT: zg.prep_joinsplit, zg.PREP_KIND_JOINSPLIT_BN: zg.prep_joinsplit_bn}
+
+
+def _prepare(jobs, ctx):
+    """-> per job: the packed 288-byte input row, or a PrepError. With a context: ONE zg_prep_batch call
+    for the window (Sapling descriptions on the GPU, JoinSplits on host threads); without: the
+    per-description host functions (in parallel for a large window)."""
+    if ctx is not None and len(jobs) >= _GPU_PREP_MIN:
+        kinds = bytes(k for k, _ in jobs)
+        fields = b"".join(zg.prep_fields(k, *a) for k, a in jobs)
+        rows, codes = ctx.prep_batch(kinds, fields)
+        return [zg.PrepError(c) if c else rows[zg.INPUT_STRIDE * i:zg.INPUT_STRIDE * (i + 1)]
+                for i, c in enumerate(codes)]
+    calls = [(_PREP_FN[k], a) for k, a in jobs]
+    if len(calls) >= _PAR_MIN:
+        done = list(_prep_pool().map(_run_prep, calls, chunksize=16))
     else:
-        done = [_run_prep(j) for j in jobs]
-    res = iter(done)
+        done = [_run_prep(c) for c in calls]
+    return [d if isinstance(d, zg.PrepError) else zg.pack_inputs([d]) for d in done]
+
+
+def _queue(txs, ctx=None):
+    """prepare inputs; returns (Groth16 items (kind, proof, 288-byte input row, n inputs), PGHR13 items
+    (proof, inputs), per-tx plans). A plan entry refers to a queued proof by index ("proof" / "pghr"),
+    or carries a prep error or a caller verdict. The window's preparation runs first (_prepare), then
+    the items and plans are assembled in reference order."""
+    res = iter(_prepare(_jobs(txs), ctx))
     items, pghr, plans = [], [], []
     for tx in txs:
         js_plan, sp_plan, out_plan = [], [], []
@@ -152,29 +182,29 @@ def _queue(txs):
             if tx.js_pubkey is None or (not d.groth and d.pghr_ok is not None):
                 js_plan.append(("caller", bool(d.pghr_ok)))
                 continue
-            inp = next(res)
-            if isinstance(inp, zg.PrepError):   # (the JoinSplit preps raise no PrepError)
-                raise inp
+            row = next(res)
+            if isinstance(row, zg.PrepError):   # (the JoinSplit preps raise no PrepError)
+                raise row
             if not d.groth:
                 js_plan.append(("pghr", len(pghr)))
-                pghr.append((bytes(d.zkproof), inp))
+                pghr.append((bytes(d.zkproof), [row[32 * j:32 * j + 32] for j in range(9)]))
                 continue
             js_plan.append(("proof", len(items)))
-            items.append((zg.KIND_SPROUT, bytes(d.zkproof), inp))
+            items.append((zg.KIND_SPROUT, bytes(d.zkproof), row, 9))
         for s in tx.spends:
-            inp = next(res)
-            if isinstance(inp, zg.PrepError):
-                sp_plan.append(("prep", inp.name))
+            row = next(res)
+            if isinstance(row, zg.PrepError):
+                sp_plan.append(("prep", row.name))
                 continue
             sp_plan.append(("proof", len(items)))
-            items.append((zg.KIND_SPEND, bytes(s.zkproof), inp))
+            items.append((zg.KIND_SPEND, bytes(s.zkproof), row, 7))
         for o in tx.outputs:
-            inp = next(res)
-            if isinstance(inp, zg.PrepError):
-                out_plan.append(("prep", inp.name))
+            row = next(res)
+            if isinstance(row, zg.PrepError):
+                out_plan.append(("prep", row.name))
                 continue
             out_plan.append(("proof", len(items)))
-            items.append((zg.KIND_OUTPUT, bytes(o.zkproof), inp))
+            items.append((zg.KIND_OUTPUT, bytes(o.zkproof), row, 5))
         plans.append((js_plan, sp_plan, out_plan))
     return items, pghr, plans
 
@@ -285,7 +315,7 @@ def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None,
     the GPU too (verify_sigs / sapling_bvk default to ctx.redjubjub_verify / ctx.sapling_bvk).
     PHGR JoinSplit proofs go through verify_pghr(proofs, inputs) -> statuses, default
     ctx.pghr13_verify (ONE zg_pghr13_verify call for the window)."""
-    items, pghr, plans = _queue(txs)
+    items, pghr, plans = _queue(txs, ctx)
     if verify is None:
         def verify(proofs, kinds, inputs, n_inputs):
             return ctx.verify_batch(proofs, kinds, inputs, n_inputs)[0]
@@ -295,10 +325,10 @@ def verify_block(txs, verify=None, ctx=None, verify_sigs=None, sapling_bvk=None,
     verify = _chunked(verify, cap)
     status = []
     if items:
-        proofs = b"".join(p for _, p, _ in items)
-        kinds = bytes(k for k, _, _ in items)
-        inputs = zg.pack_inputs([inp for _, _, inp in items])
-        n_inputs = bytes(len(inp) for _, _, inp in items)
+        proofs = b"".join(p for _, p, _, _ in items)
+        kinds = bytes(k for k, _, _, _ in items)
+        inputs = b"".join(row for _, _, row, _ in items)
+        n_inputs = bytes(nin for _, _, _, nin in items)
         status = list(verify(proofs, kinds, inputs, n_inputs))
     pghr_status = []
     if pghr:

@@ -207,6 +207,8 @@ struct zg_ctx {
   int debug_each = 0;         // ZG_DEBUG_EACH=1: every batch's statuses re-checked per proof
   uint8_t* d_dbg = nullptr;   // the per-proof statuses of that re-check
   const zg::BnKey* bn_key = nullptr;  // this slot's PGHR13 key (an immutable, reference-counted entry of the device cache)
+  uint8_t* prep_arena = nullptr;  // zg_prep_batch device buffers (grow-only)
+  size_t prep_arena_cap = 0;
   void* tree_arena = nullptr;  // zg_tree_roots scratch (grow-only, zg_merkle.hip)
   size_t tree_arena_cap = 0;
   void* bn_arena = nullptr;  // zg_pghr13_verify scratch (grow-only, zg_pghr13.hip)
@@ -420,7 +422,7 @@ extern "C" void zg_destroy(zg_ctx* ctx) {
                   ctx->d_stree, ctx->d_nodes, ctx->d_msm, ctx->d_pairf, ctx->d_ok, ctx->d_out, ctx->d_lines, ctx->d_lprod, ctx->d_fstate,
                   ctx->d_okbits, ctx->d_ptAC, ctx->d_prog, ctx->msm.count, ctx->msm.start, ctx->msm.cursor,
                   ctx->msm.entries, ctx->msm.cd, ctx->msm.seg, ctx->msm.wsum, ctx->msm.frpart, ctx->tree_arena,
-                  ctx->bn_arena, ctx->d_dbg};
+                  ctx->bn_arena, ctx->d_dbg, ctx->prep_arena};
   for (void* p : ptrs)
     if (p) hipFree(p);
   if (ctx->h_pin) hipHostFree(ctx->h_pin);
@@ -780,6 +782,8 @@ hipError_t launch_jj_comb(hipStream_t st, uint32_t* table);                     
 hipError_t launch_redjubjub(hipStream_t st, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                             const uint8_t* gen, int n, const uint32_t* comb, uint8_t* ok);
 hipError_t launch_jj_decode(hipStream_t st, const uint8_t* pts, int n, uint8_t* status, uint8_t* xy);
+hipError_t launch_prep_sapling(hipStream_t st, const uint8_t* kinds, const uint8_t* fields, int n, uint8_t* inputs,
+                               uint8_t* codes);
 hipError_t launch_sapling_bvk(hipStream_t st, int ntx, const uint32_t* off, const uint32_t* nspends,
                               const uint8_t* cvs, const int64_t* vb, const uint32_t* comb, uint8_t* bvk,
                               uint8_t* status);
@@ -1601,6 +1605,75 @@ extern "C" int zg_prep_output(const uint8_t cv[32], const uint8_t cmu[32], const
                               uint8_t inputs[5 * 32]) {
   if (!cv || !cmu || !epk || !inputs) return ZG_E_INVAL;
   return prep_output(cv, cmu, epk, inputs);
+}
+
+// A window's preparation in one call: the Sapling descriptions on the GPU (k_prep_sapling, zg_jubjub.hip),
+// the JoinSplits on host threads while it runs (BLAKE2b is host code; ~17 us each), then their rows
+// over the kernel's. Per description the same results as the single functions above (tests/
+// test_gpu_prep_batch.py): a window of 9,609 descriptions took ~380 ms through per-description host
+// calls from a Python thread pool (its per-task overhead under the GIL, not the C, was the bound).
+extern "C" int zg_prep_batch(zg_ctx* ctx, size_t n, const uint8_t* kinds, const uint8_t* fields, uint8_t* inputs,
+                             uint8_t* codes) {
+  if (!ctx || (n && (!kinds || !fields || !inputs || !codes)) || n > (1u << 26)) return ZG_E_INVAL;
+  std::vector<size_t> js;
+  size_t nsap = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (kinds[i] > ZG_PREP_KIND_JOINSPLIT_BN) return ZG_E_INVAL;
+    if (kinds[i] <= ZG_PREP_KIND_OUTPUT)
+      nsap++;
+    else
+      js.push_back(i);
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!n) return ZG_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (nsap) {  // one grow-only device buffer: kinds | fields | rows | codes
+    const size_t need = n * (2 + ZG_PREP_FIELD_BYTES + 288) + 64;
+    if (ctx->prep_arena_cap < need) {
+      if (ctx->prep_arena) HIPCHK(hipFree(ctx->prep_arena));
+      ctx->prep_arena = nullptr;
+      ctx->prep_arena_cap = 0;
+      HIPCHK(hipMalloc((void**)&ctx->prep_arena, need));
+      ctx->prep_arena_cap = need;
+    }
+    uint8_t* const dk = ctx->prep_arena;
+    uint8_t* const df = dk + n;
+    uint8_t* const din = df + (size_t)ZG_PREP_FIELD_BYTES * n;
+    uint8_t* const dc = din + (size_t)288 * n;
+    HIPCHK(hipMemcpyAsync(dk, kinds, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(df, fields, (size_t)ZG_PREP_FIELD_BYTES * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_prep_sapling(ctx->stream, dk, df, (int)n, din, dc));
+    HIPCHK(hipMemcpyAsync(inputs, din, (size_t)288 * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(codes, dc, n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  // the JoinSplits meanwhile, into their own rows (written over the copied-back buffer after the sync)
+  std::vector<uint8_t> jrows(js.size() * 288, 0);
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; k++) {
+      const uint8_t* f = fields + (size_t)ZG_PREP_FIELD_BYTES * js[k];
+      uint64_t vo = 0, vn = 0;
+      for (int b = 7; b >= 0; b--) {
+        vo = (vo << 8) | f[288 + b];
+        vn = (vn << 8) | f[296 + b];
+      }
+      prep_joinsplit_bits(f, f + 32, f + 64, f + 96, f + 128, f + 160, f + 192, f + 224, vo, vn, f + 256,
+                          kinds[js[k]] == ZG_PREP_KIND_JOINSPLIT ? 254 : 253, &jrows[288 * k]);
+    }
+  };
+  const size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), js.size() / 64 + 1});
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; t++) th.emplace_back(work, js.size() * t / nt, js.size() * (t + 1) / nt);
+  work(0, js.size() / nt);
+  for (auto& t : th) t.join();
+  if (nsap) {
+    HIPCHK(hipEventRecord(ctx->ev[13], ctx->stream));
+    HIPCHK(wait_event(ctx->ev[13]));
+  }
+  for (size_t k = 0; k < js.size(); k++) {
+    memcpy(inputs + (size_t)288 * js[k], &jrows[288 * k], 288);
+    codes[js[k]] = ZG_PREP_OK;
+  }
+  return ZG_OK;
 }
 
 extern "C" int zg_hsig(const uint8_t random_seed[32], const uint8_t nf0[32], const uint8_t nf1[32],

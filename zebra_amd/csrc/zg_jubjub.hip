@@ -117,6 +117,50 @@ __global__ void __launch_bounds__(64) k_sapling_bvk(int ntx, const uint32_t* off
   jj_write(x, y, o);
 }
 
+// Sapling public-input preparation for a window (zg_prep_batch): lane per description, kinds
+// ZG_PREP_KIND_SPEND / _OUTPUT (the JoinSplits are prepared on the host meanwhile and skipped here).
+// The same checks in the same order as prep_spend / prep_output (zg_prep.h; accept_spend
+// sapling.rs:101-155, accept_output :171-200): the first failing one is the code; every check is
+// evaluated (no early exit) so a wave's lanes stay together. Rows: 7 / 5 x 32 B LE Fr, zero padded.
+__global__ void __launch_bounds__(64) k_prep_sapling(const uint8_t* kinds, const uint8_t* fields, int n,
+                                                     uint8_t* inputs, uint8_t* codes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int kind = kinds[i];
+  if (kind != ZG_PREP_KIND_SPEND && kind != ZG_PREP_KIND_OUTPUT) return;
+  const bool spend = kind == ZG_PREP_KIND_SPEND;
+  const uint8_t* f = fields + (size_t)ZG_PREP_FIELD_BYTES * i;
+  uint8_t* out = inputs + (size_t)288 * i;
+  // points: cv (both), then rk (spend, field 3) or epk (output, field 2); the field value: anchor / cmu
+  Fr cx, cy, px, py;
+  const int c = jj_read(f, &cx, &cy) ? (jj_small_order(cx, cy) ? 2 : 0) : 1;
+  const int q = jj_read(f + (spend ? 96 : 64), &px, &py) ? (jj_small_order(px, py) ? 2 : 0) : 1;
+  Fr v;
+  const bool vin = prep_fr_from_repr(f + 32, &v);
+  int code = PREP_OK;
+  if (c == 1) code = PREP_VALUE_COMMITMENT_INVALID;
+  else if (c == 2) code = PREP_VALUE_COMMITMENT_SMALL_ORDER;
+  else if (!vin) code = spend ? PREP_ANCHOR : PREP_NOTE_COMMITMENT;
+  else if (q == 1) code = spend ? PREP_RANDOMIZED_KEY_INVALID : PREP_EPHEMERAL_KEY_INVALID;
+  else if (q == 2) code = spend ? PREP_RANDOMIZED_KEY_SMALL_ORDER : PREP_EPHEMERAL_KEY_SMALL_ORDER;
+  codes[i] = (uint8_t)code;
+  for (int b = 0; b < 288; b++) out[b] = 0;
+  if (code != PREP_OK) return;
+  // spend: rk.x rk.y cv.x cv.y anchor nf0 nf1; output: cv.x cv.y epk.x epk.y cmu
+  prep_put(out, spend ? 2 : 0, cx);
+  prep_put(out, spend ? 3 : 1, cy);
+  prep_put(out, spend ? 0 : 2, px);
+  prep_put(out, spend ? 1 : 3, py);
+  prep_fr_to_le(v, out + 32 * 4);
+  if (spend) prep_multipack_nf(f + 64, out + 32 * 5, out + 32 * 6);
+}
+
+hipError_t launch_prep_sapling(hipStream_t st, const uint8_t* kinds, const uint8_t* fields, int n, uint8_t* inputs,
+                               uint8_t* codes) {
+  hipLaunchKernelGGL(k_prep_sapling, dim3((n + 63) / 64), dim3(64), 0, st, kinds, fields, n, inputs, codes);
+  return hipGetLastError();
+}
+
 hipError_t launch_jj_comb(hipStream_t st, uint32_t* table) {
   hipLaunchKernelGGL(k_jj_comb, dim3((ZG_JJ_COMB_POINTS + 63) / 64), dim3(64), 0, st, table);
   return hipGetLastError();

@@ -22,6 +22,8 @@ KIND_NINPUTS = {KIND_SPEND: 7, KIND_OUTPUT: 5, KIND_SPROUT: 9}
 STATUS_OK, STATUS_DECODE_INVALID, STATUS_MALFORMED_VK, STATUS_VERIFY_FAILED, STATUS_INPUT_NONCANONICAL = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "DECODE_INVALID", 2: "MALFORMED_VK", 3: "VERIFY_FAILED", 4: "INPUT_NONCANONICAL"}
 PROOF_BYTES, INPUT_STRIDE, GT_BYTES, R_BYTES = 192, 288, 576, 16
+PREP_KIND_SPEND, PREP_KIND_OUTPUT, PREP_KIND_JOINSPLIT, PREP_KIND_JOINSPLIT_BN = 0, 1, 2, 3   # include/zg.h
+PREP_FIELD_BYTES = 304
 
 _lib = None
 
@@ -76,6 +78,7 @@ def lib():
         L.zg_sapling_bvk.argtypes = [vp, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), u8p,
                                      ctypes.POINTER(ctypes.c_int64), u8p, u8p]
         L.zg_jubjub_decode.argtypes = [vp, sz, u8p, u8p, u8p]
+        L.zg_prep_batch.argtypes = [vp, sz, u8p, u8p, u8p, u8p]
         L.zg_merkle_combine.argtypes = [vp, i, sz, u8p, u8p, u8p, u8p]
         L.zg_pghr13_vk_load_builtin.argtypes = [vp]
         L.zg_pghr13_vk_load_json.argtypes = [vp, u8p, sz]
@@ -119,6 +122,25 @@ def _prep(rc, out, n):
     if rc:
         raise PrepError(rc)
     return [out.raw[32 * j:32 * j + 32] for j in range(n)]
+
+
+def prep_fields(kind, *args):
+    """one description's ZG_PREP_FIELD_BYTES row for zg_prep_batch: SPEND (cv, anchor, nullifier, rk),
+    OUTPUT (cv, cmu, epk), JOINSPLIT[_BN] (anchor, random_seed, nullifiers, macs, commitments, vpub_old,
+    vpub_new, pubkey) -- the arguments of prep_spend / prep_output / prep_joinsplit[_bn]"""
+    if kind in (PREP_KIND_SPEND, PREP_KIND_OUTPUT):
+        parts = [bytes(a) for a in args]
+        if len(parts) != (4 if kind == PREP_KIND_SPEND else 3) or any(len(x) != 32 for x in parts):
+            raise ZgError(-1, "bad Sapling description fields")
+        row = b"".join(parts)
+    else:
+        anchor, seed, nfs, macs, cms, vo, vn, pk = args
+        if any(len(bytes(x)) != 32 for x in [anchor, seed, pk, *nfs, *macs, *cms]) or not (
+                len(nfs) == len(macs) == len(cms) == 2):
+            raise ZgError(-1, "bad JoinSplit description fields")
+        row = (bytes(anchor) + bytes(seed) + b"".join(map(bytes, nfs)) + b"".join(map(bytes, macs)) +
+               b"".join(map(bytes, cms)) + bytes(pk) + int(vo).to_bytes(8, "little") + int(vn).to_bytes(8, "little"))
+    return row.ljust(PREP_FIELD_BYTES, b"\0")
 
 
 def prep_spend(cv, anchor, nullifier, rk):
@@ -343,6 +365,17 @@ class Context:
         st = ctypes.create_string_buffer(max(n, 1))
         self._chk(lib().zg_sapling_bvk(self._p, n, ns, no, cvs or None, vb, bvk, st))
         return [(st.raw[i], bvk.raw[32 * i:32 * i + 32]) for i in range(n)]
+
+    def prep_batch(self, kinds, fields):
+        """zg_prep_batch: a window's public-input preparation in one call. kinds: bytes (PREP_KIND_*),
+        fields: n x PREP_FIELD_BYTES (prep_fields) -> (inputs n x 288 bytes, codes bytes: ZG_PREP_*)"""
+        n = len(kinds)
+        if len(fields) != PREP_FIELD_BYTES * n:
+            raise ZgError(-1, "fields must be n x %d bytes" % PREP_FIELD_BYTES)
+        inp = ctypes.create_string_buffer(max(INPUT_STRIDE * n, 1))
+        codes = ctypes.create_string_buffer(max(n, 1))
+        self._chk(lib().zg_prep_batch(self._p, n, bytes(kinds), bytes(fields), inp, codes))
+        return inp.raw[:INPUT_STRIDE * n], codes.raw[:n]
 
     def jubjub_decode(self, points):
         """edwards::Point::read + small-order check -> list of (status 0/1/2, x, y ints)"""
