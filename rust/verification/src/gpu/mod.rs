@@ -195,6 +195,21 @@ impl GpuVerifier {
         Ok(status)
     }
 
+    /// zg_prep_batch: a window's public-input preparation in one call (kinds ZG_PREP_KIND_*, fields
+    /// n x ZG_PREP_FIELD_BYTES; the Sapling descriptions on the GPU, the JoinSplits on host threads)
+    /// -> (inputs n x 288 bytes, codes ZG_PREP_*)
+    pub fn prep_batch(&self, kinds: &[u8], fields: &[u8]) -> Result<(Vec<u8>, Vec<u8>), GpuError> {
+        let n = kinds.len();
+        assert_eq!(fields.len(), n * ffi::ZG_PREP_FIELD_BYTES, "fields must be n x ZG_PREP_FIELD_BYTES");
+        let _g = self.lock.lock().unwrap();
+        let mut inputs = vec![0u8; ffi::ZG_INPUT_STRIDE * n];
+        let mut codes = vec![0u8; n];
+        check(self.ctx, unsafe {
+            ffi::zg_prep_batch(self.ctx, n, kinds.as_ptr(), fields.as_ptr(), inputs.as_mut_ptr(), codes.as_mut_ptr())
+        })?;
+        Ok((inputs, codes))
+    }
+
     /// binding verification keys: per tx (spend cvs, output cvs, valueBalance) -> (status, bvk)
     pub fn sapling_bvk(&self, txs: &[(Vec<[u8; 32]>, Vec<[u8; 32]>, i64)]) -> Result<Vec<(u8, [u8; 32])>, GpuError> {
         let _g = self.lock.lock().unwrap();
