@@ -277,6 +277,20 @@ def other_configs(ctx, src_proofs, src_kinds, cpu_threads=0, reps=5):
     return res
 
 
+def lineprod_parts(m, ncu, ncoeff=68, pmax=8):
+    """the step-part bounds zg.hip lineprod_parts chooses by default (wave-aligned parts) for m groups"""
+    bps = (m + 63) // 64
+    first, spw = 2 * max(1, ncu // bps), max(1, (ncu - bps) // bps)
+    ln = 2 * spw
+    while 1 + (ncoeff - min(first, ncoeff) + ln - 1) // ln > pmax:
+        ln += spw
+    b, n = [], 0
+    while n < ncoeff:
+        b.append(n)
+        n += first if len(b) == 1 else ln
+    return b + [ncoeff]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -514,8 +528,9 @@ def main():
     if os.path.exists(pmc) and shard == 65536 and not fused:   # the PMC passes run the default 64k bench
         pt = json.load(open(pmc))
         traffic, k4_traffic = pt.get(rk), pt.get("k_msm_bucket")
-        if "+" in rk:  # the line-product phase: each kernel runs once per step part (4 by default)
-            parts = int(os.environ.get("ZG_LINE_PROD_PARTS", "4"))
+        if "+" in rk:  # the line-product phase: each kernel runs once per step part
+            parts = int(os.environ.get("ZG_LINE_PROD_PARTS", "0")) or len(lineprod_parts(
+                shard // 32, torch.cuda.get_device_properties(dev).multi_processor_count)) - 1
             got = [pt.get(k) for k in rk.split("+")]
             traffic = parts * sum(got) if all(g is not None for g in got) else None
     k4 = None
