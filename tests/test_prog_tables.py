@@ -42,9 +42,10 @@ def test_prog_schedule_structure():
             assert sch["nslots"] <= 13 and nw == 4 and sch["rb"] == 1, name
             # B and C (outputs 4, 5) leave through their products' waves: no slot
             assert sorted(sch["sinks"].values()) == [4, 5], name
-        elif name in ("q4sq", "q4", "gm", "gmsq", "q4i", "q4ik"):
+        elif name in ("q4sq", "q4", "gm", "gmsq", "q4i", "q4ik", "aq4"):
             # four proofs per lane: 18 inputs fit 25 slots only with the same-round reuse (and the
-            # group chain's general products run in the same LDS budget, k_batch_fchaing)
+            # group chain's general products run in the same LDS budget, k_batch_fchaing; aq4: the
+            # affine line products of k_line_prod, round 6)
             assert sch["nslots"] <= 25 and sch["rb"] == 1, name
         else:
             # no read barrier: a slot is never written in the round that reads its previous content
