@@ -301,10 +301,16 @@ def main():
                     help="batches in flight per GPU, one context each (0: the default, 6)")
     ap.add_argument("--sync-verdict", action="store_true",
                     help="take each batch's verdict (gather + final exponentiation) before relaunching its context")
-    ap.add_argument("--checkers", type=int, default=2,
-                    help="verdict threads, one checker context each (final exponentiations of consecutive batches overlap)")
+    # (round 6) 0 = auto: two checkers in a single process (8k, 8 in flight: 2.36 vs 2.51 ms per batch with one),
+    # one under RCCL, where a second checker's high-priority stream pair beside RCCL's costs 6-13 % (8k 2.57 vs
+    # 2.79, 32k 6.69 vs 7.60 ms; profiles/r06w_rccl_priority.txt, r06y)
+    ap.add_argument("--checkers", type=int, default=0,
+                    help="verdict threads, one checker context each (final exponentiations of consecutive batches "
+                         "overlap); 0: 2, or 1 under torch.distributed")
     ap.add_argument("--no-priority", action="store_true",
                     help="default-priority streams for the checker context and RCCL")
+    ap.add_argument("--rccl-priority", choices=["high", "normal"], default="high",
+                    help="RCCL's stream priority (the checkers keep theirs unless --no-priority)")
     ap.add_argument("--dist", action="store_true", help="use torch.distributed (RCCL) even at world size 1")
     ap.add_argument("--no-iso", action="store_true", help="skip the isolated-launch pass (profiling the timed launches)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -353,7 +359,7 @@ def main():
         os.dup2(2, 1)
         try:
             opts = None
-            if not args.no_priority:   # the 576-B gathers jump the queue of in-flight batches' blocks
+            if not args.no_priority and args.rccl_priority == "high":   # the 576-B gathers jump the queue
                 opts = dist.ProcessGroupNCCL.Options()
                 opts.is_high_priority_stream = True
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), pg_options=opts)
@@ -376,7 +382,8 @@ def main():
     # statuses are read (zebra_amd.dist.run_pipelined_deferred)
     # (round 6) --checkers contexts, one per verdict thread: consecutive batches' final exponentiations
     # overlap (zebra_amd.dist.run_pipelined_deferred gather / checks)
-    checkers = [] if args.sync_verdict else [Context(device=local, max_batch=64) for _ in range(max(1, args.checkers))]
+    nck = args.checkers if args.checkers > 0 else (1 if use_dist else 2)
+    checkers = [] if args.sync_verdict else [Context(device=local, max_batch=64) for _ in range(nck)]
     for chk in checkers:
         if not args.no_priority:
             chk.set_priority(True)
@@ -464,11 +471,15 @@ def main():
     vtime.clear()
     ltime.clear()
     barrier()
+    import resource
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     results = run(args.steps)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_busy = (ru1.ru_utime - ru0.ru_utime + ru1.ru_stime - ru0.ru_stime) / dt   # CPUs busy on average
     if use_dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -582,6 +593,7 @@ def main():
         "h2d_ms_per_batch": h2d,
         "host_ms_per_batch": {"launch": 1e3 * sum(ltime) / max(1, len(ltime)), "wait_partial": host_ms[0],
                               "exchange_and_final_exp": host_ms[1], "statuses": host_ms[2],
+                              "process_cpus_busy": cpu_busy,
                               "verdict": "sync" if args.sync_verdict else
                               "deferred (ordered gather thread, %d verdict threads with a checker context each)" % len(checkers)},
     }

@@ -215,5 +215,48 @@ for s in $STEPS; do
   config5)
     timeout -k 10 300 python3 -u tools/run_config5.py ${C5ARGS:-} > $O/config5.json 2> $O/config5.err || { echo "config5 failed"; tail -30 $O/config5.err; exit 1; }
     cat $O/config5.json ;;
+  distq)
+    # the RCCL path at world size 1 (bench.py --dist) by hardware-queue count: "N:Q ..." (shard N, queues Q; 0 = bench default)
+    for cfg in ${DISTQ:-8192:0 8192:28 8192:32 65536:0}; do
+      n=${cfg%%:*}; q=${cfg##*:}; ex=""; [ "$q" != 0 ] && ex="ZG_BENCH_HWQ=$q"
+      env $ex timeout -k 10 240 python3 -u bench.py --dist --no-cpu --no-configs --no-iso --proofs $n --steps 40 > $O/dq_${n}_$q.json 2> $O/dq_${n}_$q.err || { echo "bench dist $cfg failed"; tail -20 $O/dq_${n}_$q.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/dq_${n}_$q.json')); print('dist shard $n hwq', d['config']['hw_queues'], round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s', d['config']['batches_in_flight_per_gpu'], 'in flight; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
+    done ;;
+  distx)
+    # the per-batch exchange at world size 1 under --dist: RCCL (with / without priority streams) vs no --dist
+    for n in ${SHARDS:-8192 65536}; do for x in nodist rccl rcclnp; do
+      case $x in nodist) a="";; rccl) a="--dist";; rcclnp) a="--dist --no-priority";; esac
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 40 > $O/dx_${n}_$x.json 2> $O/dx_${n}_$x.err || { echo "bench distx $n $x failed"; tail -20 $O/dx_${n}_$x.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/dx_${n}_$x.json')); print('$x shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), d['config']['collective'][:40])"
+    done; done ;;
+  distcpu)
+    # CPUs the bench process keeps busy in the timed region, --dist vs not
+    for n in ${SHARDS:-8192}; do for x in nodist rccl; do
+      a=""; [ $x = rccl ] && a="--dist"
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 100 > $O/dc_${n}_$x.json 2> $O/dc_${n}_$x.err || { echo "bench distcpu $n $x failed"; tail -20 $O/dc_${n}_$x.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/dc_${n}_$x.json')); print('$x shard $n', round(d['ms_per_step'],3), 'ms/batch; CPUs busy', round(d['host_ms_per_batch']['process_cpus_busy'],2))"
+    done; done ;;
+  distp)
+    # stream priorities under --dist (world 1), repeated: nodist / RCCL+checkers high / RCCL normal / all normal
+    for rep in 1 2; do for n in ${SHARDS:-8192 65536}; do for x in nodist hi rnorm allnorm; do
+      case $x in nodist) a="";; hi) a="--dist";; rnorm) a="--dist --rccl-priority normal";; allnorm) a="--dist --no-priority";; esac
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/dp_${n}_${x}_$rep.json 2> $O/dp_${n}_${x}_$rep.err || { echo "bench distp $n $x failed"; tail -20 $O/dp_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/dp_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
+    done; done; done ;;
+  distp2)
+    # under --dist (world 1), repeated: default / one checker / default-priority exchange stream / 32 queues / all normal + 1 checker
+    for rep in 1 2; do for n in ${SHARDS:-8192 32768}; do for x in hi ck1 xnorm q32 norm1; do
+      e=""; a="--dist"
+      case $x in ck1) a="--dist --checkers 1";; xnorm) e="ZG_XSTREAM_PRIO=0";; q32) e="ZG_BENCH_HWQ=32";; norm1) a="--dist --no-priority --checkers 1";; esac
+      env $e timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/dq_${n}_${x}_$rep.json 2> $O/dq_${n}_${x}_$rep.err || { echo "bench distp2 $n $x failed"; tail -20 $O/dq_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/dq_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
+    done; done; done ;;
+  ck8k)
+    # checkers 1 vs 2, with and without --dist, repeated (same box)
+    for rep in 1 2 3; do for n in ${SHARDS:-8192}; do for x in n1 n2 d1 d2; do
+      case $x in n1) a="--checkers 1";; n2) a="--checkers 2";; d1) a="--dist --checkers 1";; d2) a="--dist --checkers 2";; esac
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/ck_${n}_${x}_$rep.json 2> $O/ck_${n}_${x}_$rep.err || { echo "bench ck8k $n $x failed"; tail -20 $O/ck_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/ck_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
+    done; done; done ;;
   esac
 done

@@ -3,6 +3,8 @@ ROCm): contiguous shards, one 576-byte Miller partial per rank, all-gather, the 
 exponentiation of their product on every rank (same inputs, same verdict). SURVEY.md 8(e);
 DESIGN.md section 6."""
 
+import os
+
 GT_BYTES = 576
 
 
@@ -24,7 +26,9 @@ def _exchange_buffers(world, device, k):
     key = (str(device), world, k)
     if key not in _xbufs:
         gpu = torch.device(device).type == "cuda"
-        stream = torch.cuda.Stream(device=device, priority=-1) if gpu else None
+        # (ZG_XSTREAM_PRIO=0: a default-priority stream; tooling for the priority A/B of DESIGN §4d)
+        prio = -1 if os.environ.get("ZG_XSTREAM_PRIO", "1") != "0" else 0
+        stream = torch.cuda.Stream(device=device, priority=prio) if gpu else None
         _xbufs[key] = (torch.empty(k * GT_BYTES, dtype=torch.uint8, pin_memory=gpu),
                        torch.empty(k * GT_BYTES, dtype=torch.uint8, device=device),
                        torch.empty(world * k * GT_BYTES, dtype=torch.uint8, device=device),
@@ -32,7 +36,7 @@ def _exchange_buffers(world, device, k):
     return _xbufs[key]
 
 
-def combine_partials(partial, check, world, rank, device):
+def combine_partials(partial, check, world, rank, device, group=None):
     """All-gather every rank's 576-byte partial (one RCCL all-gather into one tensor, one copy
     back) and run `check(list_of_partials) -> bool` -- ONE final exponentiation of their
     product -- on every rank: all ranks hold the same partials, so they reach the same verdict
@@ -44,13 +48,14 @@ def combine_partials(partial, check, world, rank, device):
     `partial` is one 576-B partial, or a list of k of them when a rank verifies k shards of the
     batch (every rank must pass the same k): the gather then moves world x k partials in the
     same single collective, ordered rank-major (rank 0's k shards first)."""
-    return check(gather_partials(partial, world, rank, device))
+    return check(gather_partials(partial, world, rank, device, group))
 
 
-def gather_partials(partial, world, rank, device):
+def gather_partials(partial, world, rank, device, group=None):
     """The exchange step of combine_partials alone: every rank's partial(s), rank-major, as a list
     of 576-B bytes (same on every rank). Calls must not overlap and must run in the same order on
-    every rank (run_pipelined_deferred's ordered gather stage)."""
+    every rank (run_pipelined_deferred's ordered gather stage). device "cpu" with a gloo `group`
+    exchanges the host-resident partials without a device round trip (bench.py --exchange gloo)."""
     import contextlib
     import numpy as np
     import torch
@@ -62,7 +67,7 @@ def gather_partials(partial, world, rank, device):
     with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
         host.numpy()[:] = np.frombuffer(b"".join(parts), dtype=np.uint8)
         mine.copy_(host, non_blocking=True)
-        dist.all_gather_into_tensor(flat, mine)
+        dist.all_gather_into_tensor(flat, mine, group=group)
         back.copy_(flat)
     if stream is not None:
         stream.synchronize()
