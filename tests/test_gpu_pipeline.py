@@ -1,6 +1,7 @@
 """GPU tier: bench.py's default schedule (zebra_amd.dist.run_pipelined_deferred) on real contexts.
 Batch contexts are relaunched as soon as their partial and provisional statuses are read; the
-verdicts run on a worker thread on a high-priority checker context (zg_set_priority). A batch
+verdicts run off the loop: an ordered gather stage, then each final exponentiation on one of the
+high-priority checker contexts (zg_set_priority). A batch
 whose verdict is false (config 4's 41 corrupted proofs among 4,096) is re-run with bisection and
 must come back with the exact reject set; the valid batches around it are unaffected."""
 import pytest
@@ -11,15 +12,22 @@ from tests.test_gpu_parity import corrupted_4096
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("poll", [False, True], ids=["in-order", "first-ready"])
-def test_deferred_verdicts_exact_statuses(poll):
+@pytest.mark.parametrize("poll,checks", [(False, 1), (True, 1), (True, 2)],
+                         ids=["in-order", "first-ready", "first-ready-2-checkers"])
+def test_deferred_verdicts_exact_statuses(poll, checks):
+    """checks = 2: bench.py's pooled verdicts (round 6) -- the ordered gather stage, then the final
+    exponentiations on two checker contexts with their own high-priority stream pairs"""
+    import queue
     from zebra_amd import Context, pack_inputs
     from zebra_amd.dist import run_pipelined_deferred
     n = 4096
     cs = [Context(device=0, max_batch=n, seed=13) for _ in range(2)]
-    checker = Context(device=0, max_batch=64)
+    checkers = [Context(device=0, max_batch=64) for _ in range(checks)]
+    free = queue.SimpleQueue()
+    for chk in checkers:
+        chk.set_priority(True)
+        free.put(chk)
     try:
-        checker.set_priority(True)
         real = load_golden("real_proofs.json")["proofs"]
         src_proofs = b"".join(bytes.fromhex(e["proof"]) for e in real)
         src_kinds = bytes(e["kind"] for e in real)
@@ -44,8 +52,12 @@ def test_deferred_verdicts_exact_statuses(poll):
             part = c.batch_partial()
             return part, c.batch_finish(True, n)
 
-        def verdict(part):
-            return checker.gt_check([part])
+        def verdict(parts):
+            chk = free.get()
+            try:
+                return chk.gt_check(parts)
+            finally:
+                free.put(chk)
 
         def redo(s):
             c = cs[0]
@@ -54,10 +66,11 @@ def test_deferred_verdicts_exact_statuses(poll):
             return c.batch_finish(ok, n)
 
         res = run_pipelined_deferred(cs, 5, launch, harvest, verdict, redo,
-                                     ready=(lambda c: c.batch_ready()) if poll else None)
+                                     ready=(lambda c: c.batch_ready()) if poll else None,
+                                     gather=lambda part: [part], checks=checks)
         assert [ok for ok, _ in res] == [True, True, False, True, True]
         for b, (_, sts) in enumerate(res):
             assert sts == batches[b][3], b
     finally:
-        for c in cs + [checker]:
+        for c in cs + checkers:
             c.close()

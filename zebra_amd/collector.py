@@ -151,13 +151,33 @@ _PREP_FN = {zg.PREP_KIND_SPEND: zg.prep_spend, zg.PREP_KIND_OUTPUT: zg.prep_outp
             zg.PREP_KIND_JOINSPLIT: zg.prep_joinsplit, zg.PREP_KIND_JOINSPLIT_BN: zg.prep_joinsplit_bn}
 
 
+_PAD = {zg.PREP_KIND_SPEND: bytes(zg.PREP_FIELD_BYTES - 128), zg.PREP_KIND_OUTPUT: bytes(zg.PREP_FIELD_BYTES - 96)}
+
+
+def _fields(jobs):
+    """the window's zg_prep_batch field rows: the Sapling descriptions' 32-byte fields joined as they are
+    (one join for the window), the JoinSplits through zg.prep_fields; a field of the wrong size is
+    reported by zg.prep_fields"""
+    out = []
+    for k, a in jobs:
+        if k == zg.PREP_KIND_SPEND or k == zg.PREP_KIND_OUTPUT:
+            out.extend(a)
+            out.append(_PAD[k])
+        else:
+            out.append(zg.prep_fields(k, *a))
+    f = b"".join(out)
+    if len(f) != zg.PREP_FIELD_BYTES * len(jobs):
+        f = b"".join(zg.prep_fields(k, *a) for k, a in jobs)   # raises on the malformed description
+    return f
+
+
 def _prepare(jobs, ctx):
     """-> per job: the packed 288-byte input row, or a PrepError. With a context: ONE zg_prep_batch call
     for the window (Sapling descriptions on the GPU, JoinSplits on host threads); without: the
     per-description host functions (in parallel for a large window)."""
     if ctx is not None and len(jobs) >= _GPU_PREP_MIN:
         kinds = bytes(k for k, _ in jobs)
-        fields = b"".join(zg.prep_fields(k, *a) for k, a in jobs)
+        fields = _fields(jobs)
         rows, codes = ctx.prep_batch(kinds, fields)
         return [zg.PrepError(c) if c else rows[zg.INPUT_STRIDE * i:zg.INPUT_STRIDE * (i + 1)]
                 for i, c in enumerate(codes)]
