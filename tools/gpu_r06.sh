@@ -258,5 +258,12 @@ for s in $STEPS; do
       timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/ck_${n}_${x}_$rep.json 2> $O/ck_${n}_${x}_$rep.err || { echo "bench ck8k $n $x failed"; tail -20 $O/ck_${n}_${x}_$rep.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/ck_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
     done; done; done ;;
+  distshards)
+    # per-rank shard sizes of the 2/4/8-GPU line under --dist (world 1) against the single-process run, two repeats
+    for rep in 1 2; do for n in ${SHARDS:-8192 16384 32768}; do for x in nodist rccl; do
+      a=""; [ $x = rccl ] && a="--dist"
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/ds_${n}_${x}_$rep.json 2> $O/ds_${n}_${x}_$rep.err || { echo "bench distshards $n $x failed"; tail -20 $O/ds_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/ds_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch', round(d['value']), 'proofs/s;', d['config']['batches_in_flight_per_gpu'], 'in flight')"
+    done; done; done ;;
   esac
 done
