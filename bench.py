@@ -307,6 +307,14 @@ def main():
     ap.add_argument("--checkers", type=int, default=0,
                     help="verdict threads, one checker context each (final exponentiations of consecutive batches "
                          "overlap); 0: 2, or 1 under torch.distributed")
+    # (round 6) auto = on under torch.distributed, where one coalescing thread beats the single checker
+    # (8k shards 2.38-2.39 vs 2.51-2.55 ms per batch, 64k 12.12-12.21 vs 12.25-12.32) without a second
+    # high-priority stream pair beside RCCL's; in a single process it equals the two checkers (8k 2.33-2.38
+    # vs 2.36, 64k 12.19-12.27 vs 12.16-12.22; profiles/r06zc_coalesce.txt), which stay the default there
+    ap.add_argument("--coalesce", choices=["auto", "on", "off"], default="auto",
+                    help="one verdict thread that checks every gathered batch waiting for it in one launch "
+                         "(Context.gt_check_many, one final exponentiation per batch side by side) instead of "
+                         "--checkers threads; auto: on under torch.distributed")
     ap.add_argument("--no-priority", action="store_true",
                     help="default-priority streams for the checker context and RCCL")
     ap.add_argument("--rccl-priority", choices=["high", "normal"], default="high",
@@ -382,7 +390,9 @@ def main():
     # statuses are read (zebra_amd.dist.run_pipelined_deferred)
     # (round 6) --checkers contexts, one per verdict thread: consecutive batches' final exponentiations
     # overlap (zebra_amd.dist.run_pipelined_deferred gather / checks)
-    nck = args.checkers if args.checkers > 0 else (1 if use_dist else 2)
+    coalesce = (args.coalesce == "on" or (args.coalesce == "auto" and use_dist and args.checkers <= 0)) \
+        and not args.sync_verdict
+    nck = 1 if coalesce else args.checkers if args.checkers > 0 else (1 if use_dist else 2)
     checkers = [] if args.sync_verdict else [Context(device=local, max_batch=64) for _ in range(nck)]
     for chk in checkers:
         if not args.no_priority:
@@ -448,6 +458,16 @@ def main():
         vtime.append(time.perf_counter() - t0)
         return ok
 
+    vsets = []   # coalescing checker: batches per gt_check_many call
+
+    def verdict_many(sets):   # the coalescing checker: every waiting batch's final exponentiation at once
+        t0 = time.perf_counter()
+        oks = checkers[0].gt_check_many(sets)
+        dt = time.perf_counter() - t0
+        vtime.extend([dt / len(sets)] * len(sets))
+        vsets.append(len(sets))
+        return oks
+
     def redo(_s):
         launch(ctx)
         return complete(ctx)[1]
@@ -458,7 +478,8 @@ def main():
         if args.sync_verdict:
             return run_pipelined(ctxs, k, launch, complete)
         return run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=lambda c: c.batch_ready(),
-                                      gather=gather, checks=len(checkers))
+                                      gather=gather, checks=len(checkers),
+                                      verdict_many=verdict_many if coalesce else None)
 
     def barrier():
         if use_dist:
@@ -469,6 +490,7 @@ def main():
     timings.clear()
     host.clear()
     vtime.clear()
+    vsets.clear()
     ltime.clear()
     barrier()
     import resource
@@ -595,7 +617,10 @@ def main():
                               "exchange_and_final_exp": host_ms[1], "statuses": host_ms[2],
                               "process_cpus_busy": cpu_busy,
                               "verdict": "sync" if args.sync_verdict else
-                              "deferred (ordered gather thread, %d verdict threads with a checker context each)" % len(checkers)},
+                              ("deferred (ordered gather thread, one coalescing verdict thread: %.2f batches per "
+                               "gt_check_many launch)" % (sum(vsets) / max(1, len(vsets))) if coalesce else
+                               "deferred (ordered gather thread, %d verdict threads with a checker context each)"
+                               % len(checkers))},
     }
     if rank == 0 and world == 1 and not args.no_configs:
         out["other_configs"] = other_configs(ctx, src_proofs, src_kinds, 0 if args.no_cpu else cpu_threads(args.cpu_threads))

@@ -150,6 +150,11 @@ int zg_batch_partial(zg_ctx* ctx, uint8_t partial[ZG_GT_BYTES]);
  * order). */
 int zg_batch_ready(zg_ctx* ctx);
 int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok);
+/* zg_gt_check_many (round 6): the verdicts of `nsets` (1..16) batches in one launch, one final
+ * exponentiation per set, side by side on the device: set b is the next counts[b] partials of
+ * `partials` (576 B each, sum(counts) <= 4096); ok[b] = its verdict. A verdict thread that finds
+ * several batches' gathered partials waiting checks them together in the time of one. */
+int zg_gt_check_many(zg_ctx* ctx, size_t nsets, const size_t* counts, const uint8_t* partials, int* ok);
 int zg_batch_finish(zg_ctx* ctx, int batch_ok, uint8_t* status);
 /* zg_set_priority: recreate the context's two streams at the device's highest (high != 0) or
  * default priority; only between batches. A context that only runs zg_gt_check (the verdict of

@@ -98,6 +98,8 @@ extern "C" {
     pub fn zg_batch_partial(ctx: *mut ZgCtx, partial: *mut u8) -> c_int;
     pub fn zg_batch_ready(ctx: *mut ZgCtx) -> c_int;
     pub fn zg_gt_check(ctx: *mut ZgCtx, count: usize, partials: *const u8, ok: *mut c_int) -> c_int;
+    pub fn zg_gt_check_many(ctx: *mut ZgCtx, nsets: usize, counts: *const usize, partials: *const u8,
+                            ok: *mut c_int) -> c_int;
     pub fn zg_batch_finish(ctx: *mut ZgCtx, batch_ok: c_int, status: *mut u8) -> c_int;
     pub fn zg_set_priority(ctx: *mut ZgCtx, high: c_int) -> c_int;
 

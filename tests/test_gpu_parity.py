@@ -124,6 +124,16 @@ def test_split_partials(ctx):
     p2 = ctx.batch_partial()
     assert not ctx.gt_check([parts[0], p2])
     assert ctx.batch_finish(False, len(bad) + 5) == [3] * len(bad) + [0] * 5
+    # zg_gt_check_many (round 6): several batches' verdicts in one launch, each its own set -- the
+    # same verdicts as one zg_gt_check per set, a false set among true ones, 16 sets at the limit
+    sets = [parts, [parts[0], p2], parts[::-1], [parts[0], p2, parts[1]]]
+    assert ctx.gt_check_many(sets) == [ctx.gt_check(p) for p in sets] == [True, False, True, False]
+    assert ctx.gt_check_many(sets * 4) == [True, False, True, False] * 4
+    assert ctx.gt_check_many([parts]) == [True]
+    with pytest.raises(ValueError):
+        ctx.gt_check_many(sets * 5)
+    with pytest.raises(ValueError):
+        ctx.gt_check_many([parts, []])
 
 
 def test_batch_4096_one_percent_corrupted(ctx):

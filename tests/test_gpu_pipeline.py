@@ -12,11 +12,13 @@ from tests.test_gpu_parity import corrupted_4096
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("poll,checks", [(False, 1), (True, 1), (True, 2)],
-                         ids=["in-order", "first-ready", "first-ready-2-checkers"])
-def test_deferred_verdicts_exact_statuses(poll, checks):
+@pytest.mark.parametrize("poll,checks,many", [(False, 1, False), (True, 1, False), (True, 2, False),
+                                              (True, 1, True)],
+                         ids=["in-order", "first-ready", "first-ready-2-checkers", "first-ready-coalesced"])
+def test_deferred_verdicts_exact_statuses(poll, checks, many):
     """checks = 2: bench.py's pooled verdicts (round 6) -- the ordered gather stage, then the final
-    exponentiations on two checker contexts with their own high-priority stream pairs"""
+    exponentiations on two checker contexts with their own high-priority stream pairs; many: the
+    coalescing checker (bench.py --coalesce on), waiting batches' verdicts in one zg_gt_check_many"""
     import queue
     from zebra_amd import Context, pack_inputs
     from zebra_amd.dist import run_pipelined_deferred
@@ -67,7 +69,8 @@ def test_deferred_verdicts_exact_statuses(poll, checks):
 
         res = run_pipelined_deferred(cs, 5, launch, harvest, verdict, redo,
                                      ready=(lambda c: c.batch_ready()) if poll else None,
-                                     gather=lambda part: [part], checks=checks)
+                                     gather=lambda part: [part], checks=checks,
+                                     verdict_many=checkers[0].gt_check_many if many else None)
         assert [ok for ok, _ in res] == [True, True, False, True, True]
         for b, (_, sts) in enumerate(res):
             assert sts == batches[b][3], b

@@ -5,6 +5,8 @@ per-batch collectives) strictly in batch order, and return results in batch orde
 verdicts re-verified by redo."""
 import random
 
+import pytest
+
 from zebra_amd.dist import run_pipelined_deferred
 
 
@@ -101,3 +103,53 @@ def test_gather_stage_ordered_checks_overlap():
     assert peak[0] == 2
     assert [ok for ok, _ in res] == [s != 4 for s in range(10)]
     assert res[4][1] == ("redo", 4) and res[5][1] == 5
+
+
+def test_coalescing_checker_batches_waiting_sets():
+    """verdict_many (round 6): one checker thread takes every gathered set waiting for it and checks
+    them in one call -- sets coalesce while a check is running, results stay in batch order, a
+    false verdict is still re-verified, every set is checked exactly once."""
+    import time
+    ctxs = [FakeCtx(i, None) for i in range(4)]
+    seq = iter(range(100))
+    calls = []
+
+    def launch(c):
+        c.batch = next(seq)
+
+    def harvest(c):
+        return ("p", c.batch), c.batch
+
+    def gather(part):
+        return [part]
+
+    def verdict_many(sets):
+        calls.append([p[0][1] for p in sets])
+        time.sleep(0.02)                 # a final exponentiation: later batches pile up meanwhile
+        return [p[0][1] != 7 for p in sets]
+
+    def verdict(_parts):
+        raise AssertionError("the pool is not used with verdict_many")
+
+    res = run_pipelined_deferred(ctxs, 12, launch, harvest, verdict, lambda s: ("redo", s),
+                                 gather=gather, verdict_many=verdict_many, max_sets=3)
+    assert sorted(b for c in calls for b in c) == list(range(12))
+    assert all(c == sorted(c) for c in calls)
+    assert max(len(c) for c in calls) > 1 and max(len(c) for c in calls) <= 3
+    assert [ok for ok, _ in res] == [s != 7 for s in range(12)]
+    assert res[7][1] == ("redo", 7) and res[8][1] == 8
+
+
+def test_coalescing_checker_failure_reaches_every_batch():
+    ctxs = [FakeCtx(i, None) for i in range(2)]
+    seq = iter(range(100))
+
+    def launch(c):
+        c.batch = next(seq)
+
+    def verdict_many(sets):
+        raise RuntimeError("device lost")
+
+    with pytest.raises(RuntimeError, match="device lost"):
+        run_pipelined_deferred(ctxs, 4, launch, lambda c: (("p", c.batch), c.batch), None, lambda s: s,
+                               gather=lambda p: [p], verdict_many=verdict_many)

@@ -18,7 +18,7 @@ C2R = {"int": "c_int", "size_t": "usize", "uint64_t": "u64", "uint32_t": "u32", 
        "const uint8_t*": "*const u8", "uint8_t*": "*mut u8", "const void*": "*const c_void",
        "float*": "*mut f32", "double*": "*mut f64", "uint64_t*": "*mut u64", "const uint32_t*": "*const u32",
        "int*": "*mut c_int", "const int64_t*": "*const i64", "const uint64_t*": "*const u64",
-       "size_t*": "*mut usize"}
+       "size_t*": "*mut usize", "const size_t*": "*const usize"}
 
 
 def c_decls():

@@ -258,6 +258,14 @@ for s in $STEPS; do
       timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/ck_${n}_${x}_$rep.json 2> $O/ck_${n}_${x}_$rep.err || { echo "bench ck8k $n $x failed"; tail -20 $O/ck_${n}_${x}_$rep.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/ck_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3))"
     done; done; done ;;
+  coal)
+    # the coalescing checker (--coalesce on: gt_check_many) against the checker pool, single process and
+    # under --dist, alternating on one box
+    for rep in 1 2 3; do for n in ${SHARDS:-8192 65536}; do for x in n2 nc d1 dc; do
+      case $x in n2) a="--checkers 2";; nc) a="--coalesce on";; d1) a="--dist --checkers 1";; dc) a="--dist --coalesce on";; esac
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/co_${n}_${x}_$rep.json 2> $O/co_${n}_${x}_$rep.err || { echo "bench coal $n $x failed"; tail -20 $O/co_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/co_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), '|', d['config']['verdict'])"
+    done; done; done ;;
   distshards)
     # per-rank shard sizes of the 2/4/8-GPU line under --dist (world 1) against the single-process run, two repeats
     for rep in 1 2; do for n in ${SHARDS:-8192 16384 32768}; do for x in nodist rccl; do

@@ -1234,12 +1234,22 @@ extern "C" int zg_batch_ready(zg_ctx* ctx) {
   return 1;
 }
 
-extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok) {
-  if (!ctx || !partials || !ok || count == 0 || count > ZG_NODE_CHUNK) return ZG_E_INVAL;
+extern "C" int zg_gt_check_many(zg_ctx* ctx, size_t nsets, const size_t* counts, const uint8_t* partials,
+                                int* ok) {
+  if (!ctx || !counts || !partials || !ok || nsets == 0 || nsets > ZG_GT_SETS_MAX) return ZG_E_INVAL;
+  GtSets sets;
+  size_t count = 0;
+  sets.off[0] = 0;
+  for (size_t b = 0; b < nsets; b++) {
+    if (counts[b] == 0 || counts[b] > ZG_NODE_CHUNK) return ZG_E_INVAL;
+    count += counts[b];
+    if (count > ZG_NODE_CHUNK) return ZG_E_INVAL;
+    sets.off[b + 1] = (int)count;
+  }
   std::lock_guard<std::mutex> g(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   // pinned staging (asynchronous copies), then a polling wait (wait_event)
-  const size_t need = 576 * count + 64;
+  const size_t need = 576 * count + sizeof(int) * ZG_GT_SETS_MAX;
   if (ctx->h_gt_cap < need) {
     if (ctx->h_gt) HIPCHK(hipHostFree(ctx->h_gt));
     ctx->h_gt = nullptr;
@@ -1252,15 +1262,20 @@ extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, i
   hipLaunchKernelGGL(k_f12_from_bytes, dim3(nblocks(count)), dim3(ZG_BLOCK), 0, ctx->stream, ctx->d_bytes, (int)count,
                      ctx->d_pairf);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_partials_check, dim3(1), dim3(64), 0, ctx->stream, ctx->d_pairf, (int)count, ctx->d_ok,
+  hipLaunchKernelGGL(k_partials_check, dim3((unsigned)nsets), dim3(64), 0, ctx->stream, ctx->d_pairf, sets, ctx->d_ok,
                      ctx->d_out);
   HIPCHK(hipGetLastError());
   int* hok = (int*)(ctx->h_gt + 576 * count);
-  HIPCHK(hipMemcpyAsync(hok, ctx->d_ok, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(hok, ctx->d_ok, sizeof(int) * nsets, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[13], ctx->stream));
   HIPCHK(wait_event(ctx->ev[13]));
-  *ok = *hok;
+  for (size_t b = 0; b < nsets; b++) ok[b] = hok[b];
   return ZG_OK;
+}
+
+extern "C" int zg_gt_check(zg_ctx* ctx, size_t count, const uint8_t* partials, int* ok) {
+  if (!ctx || !partials || !ok || count == 0 || count > ZG_NODE_CHUNK) return ZG_E_INVAL;
+  return zg_gt_check_many(ctx, 1, &count, partials, ok);
 }
 
 // Moves the context to the device's high-priority stream pair (created once per device) or

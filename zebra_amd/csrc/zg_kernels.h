@@ -851,18 +851,25 @@ __global__ void __launch_bounds__(64) k_node_partial(BatchBufs b, NodeBufs nb) {
 }
 
 // K7 across ranks: product of partials, ONE final exponentiation (one wave), == 1 ?
-__global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, int count, int* ok, Fq12* gt) {
+// (round 6) one block per set: the verdicts of several batches (each its own set of gathered
+// partials, set b = parts[off[b] .. off[b+1])) in one launch, one wave each, side by side
+#define ZG_GT_SETS_MAX 16
+struct GtSets {
+  int off[ZG_GT_SETS_MAX + 1];
+};
+__global__ void __launch_bounds__(64) k_partials_check(const Fq12* parts, GtSets sets, int* ok, Fq12* gt) {
   __shared__ CoopWS ws;
+  const int b = blockIdx.x, lo = sets.off[b], hi = sets.off[b + 1];
   coop_init(&ws);
-  coop_load(&ws, 0, parts[0]);
-  for (int c = 1; c < count; c++) {
+  coop_load(&ws, 0, parts[lo]);
+  for (int c = lo + 1; c < hi; c++) {
     coop_load(&ws, 1, parts[c]);
     coop_mul(&ws, 0, 0, 1);
   }
   coop_final_exp(&ws, 0, 0);
-  coop_store(&ws, 0, *gt);
+  coop_store(&ws, 0, gt[b]);
   const bool one = coop_is_one(&ws, 0);
-  if (threadIdx.x == 0) *ok = one ? 1 : 0;
+  if (threadIdx.x == 0) ok[b] = one ? 1 : 0;
 }
 
 __global__ void __launch_bounds__(64) k_f12_to_bytes(const Fq12* a, int count, uint8_t* out) {

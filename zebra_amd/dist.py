@@ -92,7 +92,8 @@ def run_pipelined(ctxs, k, launch, complete):
     return out
 
 
-def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None, gather=None, checks=1):
+def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None, gather=None, checks=1,
+                           verdict_many=None, max_sets=16):
     """run_pipelined with the verdict taken off the context's critical path.
 
     harvest(ctx) -> (partial, statuses) waits for a batch's Miller partial and reads its
@@ -114,41 +115,87 @@ def run_pipelined_deferred(ctxs, k, launch, harvest, verdict, redo, ready=None, 
     exponentiation, a lone wave on the device for ~2 ms -- to a pool of `checks` threads, so the
     verdicts of consecutive batches overlap instead of bounding the batch rate (8k shards, 6 in
     flight: one verdict thread was busy 2.16 of every 2.61 ms). verdict must then be thread-safe
-    (e.g. one checker context per thread)."""
+    (e.g. one checker context per thread).
+
+    verdict_many (round 6, with gather): instead of the pool, ONE checker thread takes every
+    gathered set waiting for it (up to max_sets) and checks them together, verdict_many([partials,
+    ...]) -> [bool, ...] (Context.gt_check_many: one final exponentiation per set, side by side in one
+    launch) -- the overlap of the pool's concurrent verdicts on a single checker context."""
+    import queue
+    import threading
     import time
-    from concurrent.futures import ThreadPoolExecutor
+    from concurrent.futures import Future, ThreadPoolExecutor
     free, inflight = list(ctxs), []   # inflight: (batch index, ctx) in launch order
     done, res = {}, {}                # harvested, verdict not yet submitted / submitted
     nxt = launched = 0
-    pool = ThreadPoolExecutor(max_workers=max(1, checks)) if gather is not None else None
+    pool = coalesce = None
+    if gather is not None and verdict_many is not None:
+        coalesce = queue.SimpleQueue()   # (gathered partials, Future); None ends the checker
+
+        def checker():
+            stop = False
+            while not stop:
+                item = coalesce.get()
+                if item is None:
+                    return
+                items = [item]
+                while len(items) < max_sets:
+                    try:
+                        more = coalesce.get_nowait()
+                    except queue.Empty:
+                        break
+                    if more is None:
+                        stop = True
+                        break
+                    items.append(more)
+                try:
+                    oks = verdict_many([p for p, _ in items])
+                    for (_, f), ok in zip(items, oks):
+                        f.set_result(ok)
+                except BaseException as e:   # every waiting batch sees the failure
+                    for _, f in items:
+                        f.set_exception(e)
+        th = threading.Thread(target=checker, daemon=True)
+        th.start()
+    elif gather is not None:
+        pool = ThreadPoolExecutor(max_workers=max(1, checks))
 
     def staged(part):                 # ordered worker: the exchange, then the check on the pool
+        if coalesce is not None:
+            f = Future()
+            coalesce.put((gather(part), f))
+            return f
         return pool.submit(verdict, gather(part))
 
     def result(f):
         r = f.result()
-        return r.result() if pool is not None else r
-    with ThreadPoolExecutor(max_workers=1) as ex:
-        while launched < k or inflight:
-            while free and launched < k:
-                c = free.pop(0)
-                launch(c)
-                inflight.append((launched, c))
-                launched += 1
-            i = 0
-            if ready is not None:
-                i = next((j for j, (_, c) in enumerate(inflight) if ready(c)), None)
-                if i is None:          # nothing finished yet: poll again shortly
-                    time.sleep(2e-5)
-                    continue
-            s, c = inflight.pop(i)
-            done[s] = harvest(c)
-            free.append(c)
-            while nxt in done:         # verdicts (collectives) strictly in batch order
-                part, sts = done.pop(nxt)
-                res[nxt] = (sts, ex.submit(staged if pool is not None else verdict, part))
-                nxt += 1
-        oks = [result(res[s][1]) for s in range(k)]
-    if pool is not None:
-        pool.shutdown()
+        return r.result() if gather is not None else r
+    try:
+        with ThreadPoolExecutor(max_workers=1) as ex:
+            while launched < k or inflight:
+                while free and launched < k:
+                    c = free.pop(0)
+                    launch(c)
+                    inflight.append((launched, c))
+                    launched += 1
+                i = 0
+                if ready is not None:
+                    i = next((j for j, (_, c) in enumerate(inflight) if ready(c)), None)
+                    if i is None:          # nothing finished yet: poll again shortly
+                        time.sleep(2e-5)
+                        continue
+                s, c = inflight.pop(i)
+                done[s] = harvest(c)
+                free.append(c)
+                while nxt in done:         # verdicts (collectives) strictly in batch order
+                    part, sts = done.pop(nxt)
+                    res[nxt] = (sts, ex.submit(staged if gather is not None else verdict, part))
+                    nxt += 1
+            oks = [result(res[s][1]) for s in range(k)]
+    finally:
+        if pool is not None:
+            pool.shutdown()
+        if coalesce is not None:
+            coalesce.put(None)
+            th.join()
     return [(ok, res[s][0] if ok else redo(s)) for s, ok in enumerate(oks)]

@@ -66,6 +66,7 @@ def lib():
         L.zg_batch_partial.argtypes = [vp, u8p]
         L.zg_batch_ready.argtypes = [vp]
         L.zg_gt_check.argtypes = [vp, sz, u8p, ctypes.POINTER(i)]
+        L.zg_gt_check_many.argtypes = [vp, sz, ctypes.POINTER(sz), u8p, ctypes.POINTER(i)]
         L.zg_batch_finish.argtypes = [vp, i, u8p]
         L.zg_synth_rerandomize.argtypes = [vp, sz, u8p, u8p, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64, u8p]
         L.zg_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
@@ -306,6 +307,19 @@ class Context:
         ok = ctypes.c_int(0)
         self._chk(lib().zg_gt_check(self._p, len(partials), b"".join(partials), ctypes.byref(ok)))
         return bool(ok.value)
+
+    GT_SETS_MAX = 16
+
+    def gt_check_many(self, sets):
+        """verdicts of several batches in one launch (zg_gt_check_many): sets = [[partial, ...], ...]
+        (1..16 sets), one final exponentiation each, side by side -> [bool, ...]"""
+        n = len(sets)
+        if not 0 < n <= self.GT_SETS_MAX or any(len(p) == 0 for p in sets):
+            raise ValueError("gt_check_many: 1..%d non-empty sets" % self.GT_SETS_MAX)
+        counts = (ctypes.c_size_t * n)(*[len(p) for p in sets])
+        ok = (ctypes.c_int * n)()
+        self._chk(lib().zg_gt_check_many(self._p, n, counts, b"".join(b"".join(p) for p in sets), ok))
+        return [bool(v) for v in ok]
 
     def set_priority(self, high):
         """recreate this context's streams at the highest (True) or default priority"""
