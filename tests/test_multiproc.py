@@ -171,12 +171,13 @@ def test_pipelined_batches_world2():
         assert [e for e in log if e[0] == "done"] == [("done", b) for b in range(7)]
 
 
-def _deferred_worker(rank, world, port, q):
+def _deferred_worker(rank, world, port, q, coalesce=False):
     import sys
     import threading
+    import time
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
-    from zebra_amd.dist import combine_partials, run_pipelined_deferred
+    from zebra_amd.dist import combine_partials, gather_partials, run_pipelined_deferred
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -208,21 +209,38 @@ def _deferred_worker(rank, world, port, q):
             log.append(("redo", s))
             return ["bisected", s]
 
-        res = run_pipelined_deferred(ctxs, 7, launch, harvest, verdict, redo)
+        def gather(item):   # the ordered stage: the all-gather of batch b's partials
+            b, part = item
+            log.append(("verdict", b))
+            return b, gather_partials(part, world, rank, "cpu")
+
+        def verdict_many(sets):   # the coalescing checker: several batches' gathered sets per call
+            log.append(("check", [b for b, _ in sets]))
+            time.sleep(0.01)
+            return [all(p == _FakeCtx.partial(_Probe(b, r)) for r, p in enumerate(parts)) for b, parts in sets]
+
+        if coalesce:
+            res = run_pipelined_deferred(ctxs, 7, launch, harvest, None, redo, gather=gather,
+                                         verdict_many=verdict_many)
+        else:
+            res = run_pipelined_deferred(ctxs, 7, launch, harvest, verdict, redo)
         q.put((rank, res, log))
     finally:
         dist.destroy_process_group()
 
 
-def test_deferred_verdicts_world2():
+@pytest.mark.parametrize("coalesce", [False, True], ids=["one-verdict-thread", "gather-then-coalesced-checks"])
+def test_deferred_verdicts_world2(coalesce):
     """bench.py's default schedule: a context is relaunched right after its partial and statuses
     are read, the verdicts (the all-gather + check) run on one worker thread in batch order on
-    both ranks, and a batch with a false verdict gets redo()'s statuses on every rank"""
+    both ranks, and a batch with a false verdict gets redo()'s statuses on every rank.
+    coalesce (bench.py under torch.distributed, round 6): the all-gathers stay in batch order on the
+    ordered thread, the checks of the batches gathered meanwhile are taken together, every batch once"""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_deferred_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_deferred_worker, args=(r, 2, port, q, coalesce)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -234,9 +252,12 @@ def test_deferred_verdicts_world2():
         assert [e for e in log if e[0] == "verdict"] == [("verdict", b) for b in range(7)]
         assert [e for e in log if e[0] == "harvest"] == [("harvest", b) for b in range(7)]
         assert [e for e in log if e[0] == "redo"] == [("redo", 4)]
+        if coalesce:
+            checked = [b for e in log if e[0] == "check" for b in e[1]]
+            assert checked == list(range(7))
         # the 4th launch (batch 3) reuses the first context right after batch 0's harvest,
         # without waiting for batch 0's verdict (the worker thread logs verdicts concurrently)
-        main = [e for e in log if e[0] != "verdict"]
+        main = [e for e in log if e[0] not in ("verdict", "check")]
         assert main.index(("launch", 3)) == main.index(("harvest", 0)) + 1
 
 
