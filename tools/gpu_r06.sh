@@ -266,6 +266,17 @@ for s in $STEPS; do
       timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/co_${n}_${x}_$rep.json 2> $O/co_${n}_${x}_$rep.err || { echo "bench coal $n $x failed"; tail -20 $O/co_${n}_${x}_$rep.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/co_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), '|', d['config']['verdict'])"
     done; done; done ;;
+  depthco)
+    # batches in flight with the coalescing checker under --dist (and 64k single process), two repeats
+    for rep in 1 2; do for cfg in "8192 6" "8192 8" "8192 10" "16384 6" "16384 8" "65536 5" "65536 6" "65536 7"; do
+      set -- $cfg; n=$1; d=$2
+      for x in rccl nodist; do
+        [ $x = nodist ] && [ $n != 65536 ] && continue
+        a=""; [ $x = rccl ] && a="--dist"
+        timeout -k 10 240 python3 -u bench.py $a --inflight $d --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/dc_${n}_${d}_${x}_$rep.json 2> $O/dc_${n}_${d}_${x}_$rep.err || { echo "bench depthco $n $d $x failed"; tail -20 $O/dc_${n}_${d}_${x}_$rep.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/dc_${n}_${d}_${x}_$rep.json')); print('rep $rep $x shard $n inflight $d', round(d['ms_per_step'],3), 'ms/batch')"
+      done
+    done; done ;;
   distshards)
     # per-rank shard sizes of the 2/4/8-GPU line under --dist (world 1) against the single-process run, two repeats
     for rep in 1 2; do for n in ${SHARDS:-8192 16384 32768}; do for x in nodist rccl; do
