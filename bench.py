@@ -18,8 +18,9 @@ Batches in flight (--inflight; default 6, 8 for shards of at most 8,192 proofs):
 consecutive batches on the device, one context (buffers + streams) each. The host reads the
 oldest batch's partial and statuses and relaunches its context at once; the batch's verdict
 runs off that loop: the exchange (gather) on a worker thread in batch order, the final
-exponentiation on one of --checkers verdict threads with a checker context each, so consecutive
-verdicts overlap (--sync-verdict: before the relaunch). Every batch is fully verified and its verdict is in
+exponentiations on one coalescing verdict thread that checks every gathered batch waiting for it in
+one launch (Context.gt_check_many; --checkers N: N verdict threads with a checker context each), so
+consecutive verdicts overlap (--sync-verdict: before the relaunch). Every batch is fully verified and its verdict is in
 inside the timed region (pipeline fill and drain included); a false verdict re-runs the batch
 with bisection. A batch's own latency is phase_ms.device_pipeline plus the final exponentiation.
 """
@@ -306,15 +307,18 @@ def main():
     # 2.79, 32k 6.69 vs 7.60 ms; profiles/r06w_rccl_priority.txt, r06y)
     ap.add_argument("--checkers", type=int, default=0,
                     help="verdict threads, one checker context each (final exponentiations of consecutive batches "
-                         "overlap); 0: 2, or 1 under torch.distributed")
-    # (round 6) auto = on under torch.distributed, where one coalescing thread beats the single checker
-    # (8k shards 2.38-2.39 vs 2.51-2.55 ms per batch, 64k 12.12-12.21 vs 12.25-12.32) without a second
-    # high-priority stream pair beside RCCL's; in a single process it equals the two checkers (8k 2.33-2.38
-    # vs 2.36, 64k 12.19-12.27 vs 12.16-12.22; profiles/r06zc_coalesce.txt), which stay the default there
+                         "overlap), instead of the coalescing thread; 0: the coalescing thread, or with --coalesce "
+                         "off 2, or 1 under torch.distributed")
+    # (round 6) the coalescing checker is the default: under RCCL it beats the single checker (8k shards
+    # 2.38-2.39 vs 2.51-2.55 ms per batch, 64k 12.12-12.21 vs 12.25-12.32) without a second high-priority
+    # stream pair beside RCCL's; in a single process it ties the two-checker pool (six alternating repeats on
+    # two boxes: 8k 2.332 vs 2.343, 64k 12.246 vs 12.243 mean ms) with one checker context instead of two;
+    # at the default stream priority it is slower (8k 2.341, 64k 12.300). profiles/r06zc_coalesce.txt,
+    # r06zh_coalesce_priority.txt
     ap.add_argument("--coalesce", choices=["auto", "on", "off"], default="auto",
                     help="one verdict thread that checks every gathered batch waiting for it in one launch "
                          "(Context.gt_check_many, one final exponentiation per batch side by side) instead of "
-                         "--checkers threads; auto: on under torch.distributed")
+                         "--checkers threads; auto: on unless --checkers is given")
     ap.add_argument("--no-priority", action="store_true",
                     help="default-priority streams for the checker context and RCCL")
     ap.add_argument("--rccl-priority", choices=["high", "normal"], default="high",
@@ -390,7 +394,7 @@ def main():
     # statuses are read (zebra_amd.dist.run_pipelined_deferred)
     # (round 6) --checkers contexts, one per verdict thread: consecutive batches' final exponentiations
     # overlap (zebra_amd.dist.run_pipelined_deferred gather / checks)
-    coalesce = (args.coalesce == "on" or (args.coalesce == "auto" and use_dist and args.checkers <= 0)) \
+    coalesce = (args.coalesce == "on" or (args.coalesce == "auto" and args.checkers <= 0)) \
         and not args.sync_verdict
     nck = 1 if coalesce else args.checkers if args.checkers > 0 else (1 if use_dist else 2)
     checkers = [] if args.sync_verdict else [Context(device=local, max_batch=64) for _ in range(nck)]

@@ -266,6 +266,13 @@ for s in $STEPS; do
       timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/co_${n}_${x}_$rep.json 2> $O/co_${n}_${x}_$rep.err || { echo "bench coal $n $x failed"; tail -20 $O/co_${n}_${x}_$rep.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/co_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch; verdict ms', round(d['host_ms_per_batch']['exchange_and_final_exp'],3), '|', d['config']['verdict'])"
     done; done; done ;;
+  coprio)
+    # the coalescing checker at the default stream priority (--no-priority) vs high, single process and --dist
+    for rep in 1 2 3; do for n in ${SHARDS:-8192 65536}; do for x in n2 nc ncl dc dcl; do
+      case $x in n2) a="--checkers 2";; nc) a="--coalesce on";; ncl) a="--coalesce on --no-priority";; dc) a="--dist";; dcl) a="--dist --no-priority";; esac
+      timeout -k 10 240 python3 -u bench.py $a --no-cpu --no-configs --no-iso --proofs $n --steps 60 > $O/cp_${n}_${x}_$rep.json 2> $O/cp_${n}_${x}_$rep.err || { echo "bench coprio $n $x failed"; tail -20 $O/cp_${n}_${x}_$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/cp_${n}_${x}_$rep.json')); print('rep $rep $x shard $n', round(d['ms_per_step'],3), 'ms/batch')"
+    done; done; done ;;
   depthco)
     # batches in flight with the coalescing checker under --dist (and 64k single process), two repeats
     for rep in 1 2; do for cfg in "8192 6" "8192 8" "8192 10" "16384 6" "16384 8" "65536 5" "65536 6" "65536 7"; do
